@@ -1,0 +1,218 @@
+#!/usr/bin/env python
+"""bench.py — MCMC customer-sweeps/s of the HIP sampler on MI355X (BASELINE.json metric).
+
+One step = one sweep (z, tau, level-2 draw, 20 MH steps, storage) of every chain over every
+customer.  N=1 workload = BASELINE.json configs[1] ("c2"): bivariate M2 on the full CDNOW CBS
+(23,570 customers, covariate first_sales_scaled), 4 chains, burnin 10000 / mcmc 10000 / thin 10,
+seed 42, 20 MH steps.  --gpus N > 1 (launched by torch.distributed.run, one rank per GPU) is
+weak scaling: every rank holds one 23,570-customer CDNOW copy of a N x 23,570-customer problem
+and the ranks exchange the level-2 sufficient statistics once per sweep over RCCL.
+
+Prints ONE JSON line (rank 0).  value = chains * customers * steps / wall time of the timed
+region (max over ranks).  roofline: the sweep kernel's algorithmic bytes per launch / its mean
+launch time from HIP events recorded around every launch of the timed region.  cpu_baseline:
+the bitwise-pinned numpy restatement of the reference (oracle/ref_cpu.py) on 1 core.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+WORKLOADS = {
+    # name: (D, data, covariates, chains, burnin, mcmc, thin, draw_sink)
+    "c2": (2, "full", ["first_sales_scaled"], 4, 10000, 10000, 10, "full"),
+    "c3": (3, "full", ["gender_F", "age_scaled"], 4, 10000, 10000, 10, "full"),
+    "c1": (2, "abe", [], 4, 10000, 4000, 1, "full"),
+}
+
+
+def algorithmic_bytes(D: int, K: int, thin: int, draw_sink: str) -> float:
+    """HBM bytes one (chain, customer) moves per sweep in the sweep kernel:
+    read x (4) + t_x, T (16) + K-1 covariates (8 each) + log_s (D=3: 8) + lambda, mu (16);
+    write lambda, mu (16); level-1 draw (8(D+2)) amortised over thin when stored."""
+    rd = 4 + 16 + 8 * (K - 1) + (8 if D == 3 else 0) + 16
+    wr = 16
+    draws = 8.0 * (D + 2) / thin if draw_sink == "full" else (8.0 * 2 * (7 if D == 2 else 9) / thin if draw_sink == "summary" else 0.0)
+    return rd + wr + draws
+
+
+def load_workload(name: str):
+    import numpy as np
+    import pandas as pd
+    from mcmc_clv_model_amd.data import add_driver_columns
+    D, data, covs, chains, burnin, mcmc, thin, sink = WORKLOADS[name]
+    d = np.load(os.path.join(ROOT, "tests", "golden", f"cdnow_{data}_cbs.npz"), allow_pickle=False)
+    df = add_driver_columns(pd.DataFrame({k: d[k] for k in d.files}))
+    return df, D, covs, chains, burnin, mcmc, thin, sink
+
+
+def cpu_baseline_child(workload: str, warm: int, timed: int) -> None:
+    """Runs in a fresh process with OMP/OPENBLAS threads = 1: the oracle (numpy port of the
+    reference, bitwise equal to it) sweeping 1 chain of the workload."""
+    import numpy as np
+    from oracle import ref_cpu as orc
+    df, D, covs, chains, burnin, mcmc, thin, sink = load_workload(workload)
+    cbs, X = orc.design_matrix(df, covs)
+    K = X.shape[1]
+    hyper = orc.default_hyper(K, D)
+    stamps = {}
+
+    def on_sweep(step):
+        if step in (warm, warm + timed):
+            stamps[step] = time.perf_counter()
+
+    stream = orc.Stream(np.random.default_rng(42))
+    x, t_x, T = cbs["x"].to_numpy(), cbs["t_x"].to_numpy(), cbs["T_cal"].to_numpy()
+    if D == 2:
+        orc.run_chain_bi(1, x, t_x, T, X, hyper, mcmc, burnin, thin, stream, 0, 20, n_sweeps=warm + timed,
+                         on_sweep=on_sweep)
+    else:
+        orc.run_chain_tri(1, x, t_x, T, cbs["log_s"].to_numpy(), X, hyper, mcmc, burnin, thin, stream, 0, 20,
+                          n_sweeps=warm + timed, omega2=cbs["log_s"].var(), log_s_mean=cbs["log_s"].mean(),
+                          on_sweep=on_sweep)
+    dt = stamps[warm + timed] - stamps[warm]
+    print(json.dumps(dict(s_per_sweep=dt / timed, value=len(df) * timed / dt)))
+
+
+def cpu_baseline(workload: str, warm: int = 20, timed: int = 200):
+    env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1",
+               HIP_VISIBLE_DEVICES="", ROCR_VISIBLE_DEVICES="")
+    out = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-baseline-child", "--workload", workload,
+                          "--cpu-warm", str(warm), "--cpu-timed", str(timed)],
+                         capture_output=True, text=True, env=env, check=True, timeout=900)
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    n = len(load_workload(workload)[0])
+    return dict(value=r["value"], unit="customer-sweeps/s", cores=1, kind="port",
+                s_per_sweep=r["s_per_sweep"],
+                sample=f"oracle/ref_cpu.py (numpy restatement, bitwise equal to the reference) on {workload}: "
+                       f"1 chain x {n} customers, {timed} timed sweeps after {warm} warm-up sweeps, 1 thread")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=19000)
+    ap.add_argument("--warmup", type=int, default=1000)
+    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-timing", action="store_true",
+                    help="replay captured hipGraphs in the timed region instead of event-timed launches")
+    ap.add_argument("--cpu-baseline-child", action="store_true")
+    ap.add_argument("--cpu-warm", type=int, default=20)
+    ap.add_argument("--cpu-timed", type=int, default=200)
+    a = ap.parse_args()
+    if a.cpu_baseline_child:
+        cpu_baseline_child(a.workload, a.cpu_warm, a.cpu_timed)
+        return
+
+    import numpy as np
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
+
+    from mcmc_clv_model_amd import _lib
+    from mcmc_clv_model_amd.sampler import HipSampler, build_problem
+
+    df, D, covs, chains, burnin, mcmc, thin, sink = load_workload(a.workload)
+    total = a.warmup + a.steps
+    mcmc = max(mcmc, total - burnin)
+    n_per_rank = len(df)
+    if world == 1:
+        p = build_problem(df, covs, D)
+        s = HipSampler(p, mcmc=mcmc, burnin=burnin, thin=thin, chains=chains, seed=42, draw_sink=sink,
+                       device=local_rank)
+        run = s.run
+        sync = s.synchronize
+        kern = s
+    else:
+        import pandas as pd
+        from mcmc_clv_model_amd.distributed import ShardedSampler
+        tiled = pd.concat([df] * world, ignore_index=True)
+        p = build_problem(tiled, covs, D)
+        ss = ShardedSampler(p, rank=rank, world=world, chains=chains, mcmc=mcmc, burnin=burnin, thin=thin, seed=42,
+                            draw_sink=sink, device=local_rank)
+        run = ss.step
+        sync = ss.synchronize
+        kern = ss.s
+
+    K = len(covs) + 1
+    timing = not a.no_kernel_timing and world == 1
+    run(a.warmup)
+    sync()
+    if timing:
+        kern.set_timing(True)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(a.steps)
+    sync()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    units = chains * n_per_rank * world * a.steps
+    value = units / dt
+
+    roofline = None
+    kt = kern.kernel_time() if timing else None
+    bpu = algorithmic_bytes(D, K, thin, sink)
+    if kt and kt["sweep_launches"]:
+        t_launch = kt["sweep_ms"] / kt["sweep_launches"] * 1e-3
+        achieved = bpu * chains * n_per_rank / t_launch / 1e9
+        roofline = dict(bound="hbm", achieved=round(achieved, 3), peak=HBM_PEAK_GBS, unit="GB/s",
+                        frac=round(achieved / HBM_PEAK_GBS, 6), traffic=None,
+                        kernel="sweep_kernel", bytes_per_unit=bpu,
+                        units_per_launch=chains * n_per_rank,
+                        sweep_kernel_us=round(t_launch * 1e6, 3),
+                        hyper_kernel_us=round(kt["hyper_ms"] / max(kt["hyper_launches"], 1) * 1e3, 3),
+                        launches=kt["sweep_launches"])
+
+    if rank == 0:
+        cpu = None
+        if world == 1 and not a.no_cpu_baseline:
+            cpu = cpu_baseline(a.workload)
+        wl = WORKLOADS[a.workload]
+        line = dict(
+            metric="MCMC sweeps/sec x N_customers (customer-sweeps/s)", value=value, unit="customer-sweeps/s",
+            n_gpus=world, steps=a.steps, warmup=a.warmup, ms_per_step=dt / a.steps * 1e3, higher_is_better=True,
+            scaling="weak", vs_baseline=None, dtype="f64",
+            data="CDNOW full CBS (23,570 real customers, tests/golden/cdnow_full_cbs.npz)"
+                 + ("" if world == 1 else f", tiled x{world} (one copy per rank)"),
+            config=dict(workload=f"{a.workload}: {'bivariate' if D == 2 else 'trivariate'} M2, covariates {covs}",
+                        n_customers=n_per_rank * world, chains=chains, n_mh_steps=20, burnin=burnin, mcmc=mcmc,
+                        thin=thin, seed=42, draw_sink=sink, parallelism=f"customer-shard x{world}",
+                        timed_region="event-timed launches" if timing else "hipGraph replay"),
+            roofline=roofline, cpu_baseline=cpu,
+            speedup_vs_cpu_1core=(value / cpu["value"]) if cpu else None,
+        )
+        print(json.dumps(line))
+    kern.close() if world == 1 else ss.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

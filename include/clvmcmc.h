@@ -1,0 +1,177 @@
+/*
+ * clvmcmc.h — C ABI of the MI355X-native Gibbs/MH sampler for the Abe (2009/2015)
+ * hierarchical Pareto/NBD model (libclvmcmc.so, built from mcmc_clv_model_amd/csrc/).
+ *
+ * The reference (lucagem29/mcmc_clv_model) is pure Python and has no FFI of its own;
+ * its drop-in boundary is the Python function pair
+ *     src/models/bivariate/mcmc.py:437   mcmc_draw_parameters(...)
+ *     src/models/trivariate/mcmc.py:580  mcmc_draw_parameters_rfm_m(...)
+ * The Python host (mcmc_clv_model_amd/bivariate.py, trivariate.py) keeps those
+ * signatures and binds the entry points below with ctypes.
+ * Each entry point names the reference code it replaces.
+ *
+ * Conventions
+ *  - Every function returns 0 on success or a negative CLV_E* code; the message of the
+ *    last failure on the calling thread is available from clv_last_error().
+ *  - Inputs are copied to device memory by clv_create(); outputs are written into
+ *    caller-owned, contiguous, preallocated host buffers (float64, C order).
+ *  - A sampler handle belongs to one host thread and one HIP device.
+ *  - Customer data is struct-of-arrays: one contiguous array per CBS column.
+ *  - All hot-path arithmetic is float64, like the reference; Philox proposal noise is
+ *    generated in float32.
+ */
+#ifndef CLVMCMC_H
+#define CLVMCMC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CLV_ABI_VERSION 1
+
+/* Customers per workgroup == the sufficient-statistic block size. Shards must begin on a
+ * multiple of it so block partial sums are identical for every GPU count. */
+#define CLV_BLOCK 256
+#define CLV_MAX_K 9
+#define CLV_MAX_D 3
+
+enum { CLV_OK = 0, CLV_EINVAL = -1, CLV_EHIP = -2, CLV_ESTATE = -3, CLV_ENOMEM = -4 };
+enum { CLV_RNG_PHILOX = 0, CLV_RNG_REPLAY = 1 };
+enum { CLV_SINK_FULL = 0, CLV_SINK_SUMMARY = 1, CLV_SINK_NONE = 2 };
+
+/* Per-customer running sums kept on device by CLV_SINK_SUMMARY (and readable in any mode),
+ * accumulated over stored draws. Layout of clv_read_summary(): [chain][stat][n]. */
+enum {
+  CLV_SUM_LAMBDA = 0, CLV_SUM_MU, CLV_SUM_Z, CLV_SUM_LOG_LAMBDA, CLV_SUM_LOG_MU,
+  CLV_SUM_LAMBDA2, CLV_SUM_MU2, CLV_SUM_ETA, CLV_SUM_LOG_ETA, CLV_N_SUM_STATS
+};
+
+typedef struct clv_config {
+  int32_t abi_version;   /* must equal CLV_ABI_VERSION */
+  int32_t D;             /* 2 = bivariate (bivariate/mcmc.py), 3 = trivariate (trivariate/mcmc.py) */
+  int32_t K;             /* design-matrix columns incl. the intercept, 1..CLV_MAX_K (bi:467-470) */
+  int32_t n_mh_steps;    /* MH steps per sweep (bi:278, default 20) */
+  int32_t burnin, mcmc, thin;          /* bi:437-447 semantics */
+  int32_t n_chains;      /* chains batched into one launch (reference: sequential, bi:485) */
+  int32_t chain_first;   /* global index of chain 0 of this handle: Philox key = seed + chain */
+  int32_t rng_mode;      /* CLV_RNG_PHILOX or CLV_RNG_REPLAY (test mode, clv_set_replay_tape) */
+  int32_t draw_sink;     /* CLV_SINK_* */
+  int32_t device;        /* HIP device ordinal, -1 = current device */
+  uint64_t seed;         /* Philox key base (reference: default_rng(seed + chain), bi:486) */
+  int64_t n_global;      /* customers in the whole problem (nu_n and the log-lik mean use it) */
+  int64_t shard_begin;   /* global index of this shard's first customer, multiple of CLV_BLOCK */
+  int32_t world_size;    /* shards (one process per GPU); 1 = unsharded */
+  int32_t rank;          /* this shard */
+  int32_t blocks_per_rank; /* blocks of CLV_BLOCK customers per shard (last shard may be short);
+                              0 = derive (unsharded only) */
+  int32_t blocks_per_unit; /* blocks whose partials are summed into one exchanged unit (power of
+                              two, a function of n_global only so every world size sums alike);
+                              0 = derive with clv_default_blocks_per_unit(n_global) */
+  uint64_t stream;       /* hipStream_t to launch on; 0 = a stream owned by the sampler */
+} clv_config;
+
+typedef struct clv_data {
+  int64_t n;                 /* customers in this shard */
+  const int32_t* x;          /* repeat transactions (bi:280) */
+  const double* t_x;         /* recency (bi:194) */
+  const double* T_cal;       /* calibration length (bi:194) */
+  const double* covariates;  /* (K-1) arrays of n doubles, one per non-intercept column; NULL if K==1 */
+  const double* log_s;       /* log average spend, D==3 only (tri:329) */
+} clv_data;
+
+/* Host-computed constants; the reference computes the same quantities on the host. */
+typedef struct clv_prior {
+  double lam_init;           /* bi:368 */
+  double V[CLV_MAX_K * CLV_MAX_K];       /* inv(X'X + A0), K x K row-major (bi:248-249; constant) */
+  double chol_V[CLV_MAX_K * CLV_MAX_K];  /* lower Cholesky factor of V */
+  double A0B0[CLV_MAX_K * CLV_MAX_D];    /* A0 @ B0, K x D row-major (bi:250) */
+  double S0_B0A0B0[CLV_MAX_D * CLV_MAX_D]; /* S0 + B0' A0 B0, D x D (bi:255 after expansion) */
+  double nu_n;               /* nu0 + n_global (bi:256) */
+  double beta_init[CLV_MAX_K * CLV_MAX_D]; /* tri: beta used by sweep 1 = beta_0 (tri:504) */
+  double sigma_init[CLV_MAX_D * CLV_MAX_D];/* tri: Sigma used by sweep 1 = gamma_00 (tri:504) */
+  double omega2;             /* tri: var(log_s, ddof=1) (tri:494) */
+} clv_prior;
+
+typedef struct clv_sampler clv_sampler;
+
+int32_t clv_abi_version(void);
+int32_t clv_default_blocks_per_unit(int64_t n_global);
+/* sizeof(clv_config), sizeof(clv_data), sizeof(clv_prior) for which = 0, 1, 2 (binding checks). */
+int64_t clv_sizeof(int32_t which);
+const char* clv_last_error(void);
+int clv_device_count(int32_t* count);
+
+/* Allocate device state, upload the shard, initialise lambda/mu (bi:367-379, tri:488-504) and,
+ * for D==2, the block partial sums the first level-2 draw needs. Replaces the setup half of
+ * _run_chain (bi:346-382, tri:465-507). */
+int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* prior,
+               clv_sampler** out);
+void clv_destroy(clv_sampler* s);
+
+/* Test mode (CLV_RNG_REPLAY): variates recorded from the reference's numpy Generator.
+ * Per chain, per sweep: [u_z n][v_tau n][S x (t_l n, t_m n, u_acc n)][eta_z n if D==3]
+ * [hyper 40: iw_normal(3) iw_chi2(3) mvn_noise(<=27) pad]; chains back to back. */
+int clv_set_replay_tape(clv_sampler* s, const double* tape, int64_t n_sweeps);
+int64_t clv_replay_sweep_stride(const clv_sampler* s);
+
+/* Run n sweeps (unsharded: world_size == 1). One sweep = a6's loop body: z (bi:388),
+ * tau (bi:390), level-2 (bi:393), level-1 MH (bi:396), eta (tri:524-526), storage (bi:402-428).
+ * Synchronous; chunks of sweeps are replayed from a captured hipGraph. */
+int clv_run(clv_sampler* s, int64_t n_sweeps);
+
+/* Sharded stepping (one process per GPU; the caller exchanges the unit partials over RCCL):
+ *   after clv_create, bivariate only: [exchange] clv_hyper   (initial draw, bi:393 of sweep 1)
+ *   per sweep:                        clv_sweep, [exchange] clv_hyper
+ * (bivariate: the hyper after sweep s is bi:393 of sweep s+1; trivariate: tri:529 of sweep s).
+ * clv_partials() exposes this shard's unit partials, [chain][units_per_rank][stride] doubles;
+ * clv_hyper() reads the gathered buffer [world][chain][units_per_rank][stride]
+ * (NULL = the local buffer, world_size == 1) and sums it in global unit order. */
+int clv_sweep(clv_sampler* s);
+int clv_hyper(clv_sampler* s, const double* gathered_device_ptr);
+int clv_partials(clv_sampler* s, double** device_ptr, int64_t* n_doubles, int32_t* stride);
+/* Device-to-device copy of this shard's unit partials into dst (on the sampler's stream). */
+int clv_copy_partials(clv_sampler* s, void* dst_device_ptr);
+int clv_synchronize(clv_sampler* s);
+int64_t clv_sweeps_done(const clv_sampler* s);
+
+/* Outputs. level1: [chain][draw][n][D+2] (lambda, mu, tau, z, [eta]) — bi:407-410, tri:544-548;
+ * level2: [chain][draw][D*K + D(D+1)/2] — bi:411-412, tri:549-554;
+ * loglik: [chain][draw] per-draw mean of the likelihood term — bi:423-428.
+ * Any pointer may be NULL. level1 requires draw_sink == CLV_SINK_FULL. */
+int clv_read_draws(clv_sampler* s, double* level1, double* level2, double* loglik);
+/* [chain][CLV_N_SUM_STATS][n] running sums over stored draws, and the number of stored draws. */
+int clv_read_summary(clv_sampler* s, double* sums, int64_t* n_stored);
+
+/* Current state: lambda, mu [chain][n]; hyper [chain][beta K*D, Sigma D*D]. Setting the state
+ * is exact resume (the Philox counter is the sweep index). */
+int clv_get_state(clv_sampler* s, double* lambdas, double* mus, double* hyper);
+int clv_set_state(clv_sampler* s, const double* lambdas, const double* mus, const double* hyper,
+                  int64_t sweeps_done);
+
+/* Per-launch timing of the sweep kernel with HIP events on the launch stream. */
+int clv_set_timing(clv_sampler* s, int32_t enable);
+int clv_kernel_time(clv_sampler* s, double* sweep_kernel_ms_total, int64_t* sweep_launches,
+                    double* hyper_kernel_ms_total, int64_t* hyper_launches);
+
+/* ---- test hooks (run the device code paths on caller data) ---- */
+/* Philox4x32-10 on device: ctr/out are n x 4 words. */
+int clv_debug_philox(uint32_t k0, uint32_t k1, const uint32_t* ctr, int64_t n, uint32_t* out);
+/* The Philox-mode variates of one sweep for customers [0, n): t_l/t_m/u_acc are S x n. */
+int clv_debug_variates(uint64_t seed, int32_t chain, uint32_t sweep, int64_t n, int32_t n_steps,
+                       float* t_l, float* t_m, float* u_acc, double* u_z, double* u_tau,
+                       double* e_alive, double* eta_z);
+/* Level-2 draw from given sufficient statistics and variates (replaces bi:233-262 given rng):
+ * xty K*D, yty D*D, iw_normal n_tril, iw_chi2 D, z D*K (standard normals) -> beta, Sigma. */
+int clv_debug_level2(int32_t D, int32_t K, const clv_prior* prior, const double* xty,
+                     const double* yty, const double* iw_normal, const double* iw_chi2,
+                     const double* z, double* beta, double* sigma);
+/* Philox-mode chi-square and normal draws of the hyper stream (n of each). */
+int clv_debug_hyper_variates(uint64_t seed, int32_t chain, uint32_t sweep, double df, int64_t n,
+                             double* chi2, double* normals);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CLVMCMC_H */

@@ -1,0 +1,727 @@
+// C ABI of libclvmcmc.so (declared in include/clvmcmc.h): device memory, the sweep pipeline,
+// hipGraph capture of sweep chunks, and outputs.  Host-side replacement of _run_chain /
+// mcmc_draw_parameters (src/models/bivariate/mcmc.py:346-504, trivariate/mcmc.py:465-657).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "kernels.h"
+#include "philox.h"
+
+using namespace clv;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define CLV_HIP(expr)                                                                           \
+  do {                                                                                          \
+    hipError_t e_ = (expr);                                                                     \
+    if (e_ != hipSuccess)                                                                       \
+      return fail(CLV_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_));                 \
+  } while (0)
+
+template <class T>
+hipError_t dalloc(T** p, size_t count) {
+  *p = nullptr;
+  if (count == 0) return hipSuccess;
+  return hipMalloc((void**)p, count * sizeof(T));
+}
+
+constexpr int PRIOR_DOUBLES = 81 + 81 + 27 + 9;  // V, cholV, A0B0, S0B
+constexpr int GRAPH_CHUNK = 64;                  // sweeps per captured graph
+constexpr int TIMING_EVENTS = 256;               // sweep launches timed per harvest
+
+}  // namespace
+
+struct clv_sampler {
+  clv_config cfg{};
+  clv_prior prior{};
+  Geometry g{};
+  bool replay = false;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+
+  int32_t* d_x = nullptr;
+  double *d_tx = nullptr, *d_T = nullptr, *d_cov = nullptr, *d_logs = nullptr;
+  double *d_lam = nullptr, *d_mu = nullptr, *d_hyper = nullptr;
+  double *d_block = nullptr, *d_unit = nullptr;
+  double* d_prior = nullptr;
+  Ctrl* d_ctrl = nullptr;
+  double *d_level1 = nullptr, *d_level2 = nullptr, *d_loglik = nullptr, *d_sums = nullptr;
+  double* d_tape = nullptr;
+  double* d_bs = nullptr;  // staging for set_hyper
+  int64_t tape_sweeps = 0;
+
+  bool pending_init_hyper = false;  // bivariate: the draw for sweep 1 is still due
+  int64_t sweeps_done = 0;
+
+  hipGraphExec_t graph_exec = nullptr;
+  int graph_sweeps = 0;
+
+  bool timing = false;
+  std::vector<hipEvent_t> ev;  // 4 per slot: sweep start/end, hyper start/end
+  int ev_used = 0;
+  double t_sweep_ms = 0.0, t_hyper_ms = 0.0;
+  int64_t n_sweep_timed = 0, n_hyper_timed = 0;
+};
+
+namespace {
+
+SweepArgs sweep_args(clv_sampler* s, int init) {
+  SweepArgs a{};
+  a.g = s->g;
+  a.r.seed = s->cfg.seed;
+  a.r.chain_first = s->cfg.chain_first;
+  a.r.tape = s->d_tape;
+  a.r.tape_sweep_stride = clv_replay_sweep_stride(s);
+  a.r.tape_sweeps = s->tape_sweeps;
+  a.x = s->d_x;
+  a.tx = s->d_tx;
+  a.T = s->d_T;
+  a.cov = s->d_cov;
+  a.log_s = s->d_logs;
+  a.lam = s->d_lam;
+  a.mu = s->d_mu;
+  a.hyper = s->d_hyper;
+  a.blockpart = s->d_block;
+  a.ctrl = s->d_ctrl;
+  a.level1 = s->d_level1;
+  a.sums = s->d_sums;
+  a.n_stored = nullptr;
+  a.lam_init = s->prior.lam_init;
+  a.init = init;
+  return a;
+}
+
+HyperArgs hyper_args(clv_sampler* s, const double* units, int mode) {
+  HyperArgs a{};
+  a.g = s->g;
+  a.r.seed = s->cfg.seed;
+  a.r.chain_first = s->cfg.chain_first;
+  a.r.tape = s->d_tape;
+  a.r.tape_sweep_stride = clv_replay_sweep_stride(s);
+  a.r.tape_sweeps = s->tape_sweeps;
+  a.units = units ? units : s->d_unit;
+  a.hyper = s->d_hyper;
+  a.ctrl = s->d_ctrl;
+  a.level2 = s->d_level2;
+  a.loglik = s->d_loglik;
+  a.V = s->d_prior;
+  a.cholV = s->d_prior + 81;
+  a.A0B0 = s->d_prior + 162;
+  a.S0B = s->d_prior + 189;
+  a.nu_n = s->prior.nu_n;
+  a.omega2 = s->prior.omega2;
+  a.mode = mode;
+  return a;
+}
+
+int enqueue_sweep(clv_sampler* s, hipEvent_t e0, hipEvent_t e1) {
+  if (e0) CLV_HIP(hipEventRecord(e0, s->stream));
+  CLV_HIP(launch_sweep(sweep_args(s, 0), s->replay, s->stream));
+  if (e1) CLV_HIP(hipEventRecord(e1, s->stream));
+  if (s->g.blocks_per_unit > 1) {
+    GroupArgs ga{};
+    ga.g = s->g;
+    ga.blockpart = s->d_block;
+    ga.unitpart = s->d_unit;
+    CLV_HIP(launch_group(ga, s->stream));
+  }
+  return CLV_OK;
+}
+
+int enqueue_hyper(clv_sampler* s, const double* units, int mode, hipEvent_t e0, hipEvent_t e1) {
+  if (e0) CLV_HIP(hipEventRecord(e0, s->stream));
+  CLV_HIP(launch_hyper(hyper_args(s, units, mode), s->replay, s->stream));
+  if (e1) CLV_HIP(hipEventRecord(e1, s->stream));
+  return CLV_OK;
+}
+
+int check_replay_range(clv_sampler* s, int64_t n_more) {
+  if (!s->replay) return CLV_OK;
+  const int64_t need = s->sweeps_done + n_more + (s->g.D == 2 ? 1 : 0);
+  if (!s->d_tape || need > s->tape_sweeps)
+    return fail(CLV_ESTATE, "replay tape too short: need " + std::to_string(need) + " sweeps, have " +
+                                std::to_string(s->tape_sweeps));
+  return CLV_OK;
+}
+
+int harvest_timing(clv_sampler* s) {
+  if (s->ev_used == 0) return CLV_OK;
+  CLV_HIP(hipEventSynchronize(s->ev[4 * s->ev_used - 1]));
+  for (int k = 0; k < s->ev_used; ++k) {
+    float ms = 0.f;
+    CLV_HIP(hipEventElapsedTime(&ms, s->ev[4 * k], s->ev[4 * k + 1]));
+    s->t_sweep_ms += ms;
+    s->n_sweep_timed++;
+    CLV_HIP(hipEventElapsedTime(&ms, s->ev[4 * k + 2], s->ev[4 * k + 3]));
+    s->t_hyper_ms += ms;
+    s->n_hyper_timed++;
+  }
+  s->ev_used = 0;
+  return CLV_OK;
+}
+
+int build_graph(clv_sampler* s, int n) {
+  if (s->graph_exec && s->graph_sweeps == n) return CLV_OK;
+  if (s->graph_exec) {
+    CLV_HIP(hipGraphExecDestroy(s->graph_exec));
+    s->graph_exec = nullptr;
+  }
+  hipGraph_t graph;
+  CLV_HIP(hipStreamBeginCapture(s->stream, hipStreamCaptureModeThreadLocal));
+  for (int k = 0; k < n; ++k) {
+    int rc = enqueue_sweep(s, nullptr, nullptr);
+    if (rc == CLV_OK) rc = enqueue_hyper(s, nullptr, 0, nullptr, nullptr);
+    if (rc != CLV_OK) {
+      hipGraph_t dummy;
+      (void)hipStreamEndCapture(s->stream, &dummy);
+      return rc;
+    }
+  }
+  CLV_HIP(hipStreamEndCapture(s->stream, &graph));
+  CLV_HIP(hipGraphInstantiate(&s->graph_exec, graph, nullptr, nullptr, 0));
+  CLV_HIP(hipGraphDestroy(graph));
+  s->graph_sweeps = n;
+  return CLV_OK;
+}
+
+bool is_pow2(int v) { return v > 0 && (v & (v - 1)) == 0; }
+
+}  // namespace
+
+extern "C" {
+
+int32_t clv_abi_version(void) { return CLV_ABI_VERSION; }
+
+int32_t clv_default_blocks_per_unit(int64_t n_global) {
+  // Keep the number of exchanged/reduced units <= 512 (one hyper workgroup sums them).
+  const int64_t nb = (n_global + BLOCK - 1) / BLOCK;
+  int32_t g = 1;
+  while ((nb + g - 1) / g > 512) g *= 2;
+  return g;
+}
+
+const char* clv_last_error(void) { return g_err.c_str(); }
+
+int64_t clv_sizeof(int32_t which) {
+  switch (which) {
+    case 0: return (int64_t)sizeof(clv_config);
+    case 1: return (int64_t)sizeof(clv_data);
+    case 2: return (int64_t)sizeof(clv_prior);
+    default: return -1;
+  }
+}
+
+int clv_device_count(int32_t* count) {
+  int n = 0;
+  CLV_HIP(hipGetDeviceCount(&n));
+  *count = n;
+  return CLV_OK;
+}
+
+int64_t clv_replay_sweep_stride(const clv_sampler* s) {
+  const int64_t n = s->g.n;
+  return n * (2 + 3 * (int64_t)s->g.S + (s->g.D == 3 ? 1 : 0)) + TAPE_HYPER;
+}
+
+int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* prior, clv_sampler** out) {
+  if (!cfg || !data || !prior || !out) return fail(CLV_EINVAL, "null argument");
+  *out = nullptr;
+  if (cfg->abi_version != CLV_ABI_VERSION) return fail(CLV_EINVAL, "ABI version mismatch");
+  if (cfg->D != 2 && cfg->D != 3) return fail(CLV_EINVAL, "D must be 2 or 3");
+  if (cfg->K < 1 || cfg->K > CLV_MAX_K) return fail(CLV_EINVAL, "K must be in 1..9");
+  if (cfg->n_mh_steps < 0) return fail(CLV_EINVAL, "n_mh_steps must be >= 0");
+  if (cfg->thin < 1) return fail(CLV_EINVAL, "thin must be >= 1");
+  if (cfg->burnin < 0 || cfg->mcmc < 0) return fail(CLV_EINVAL, "burnin/mcmc must be >= 0");
+  if (cfg->n_chains < 1) return fail(CLV_EINVAL, "n_chains must be >= 1");
+  if (cfg->rng_mode != CLV_RNG_PHILOX && cfg->rng_mode != CLV_RNG_REPLAY) return fail(CLV_EINVAL, "bad rng_mode");
+  if (cfg->draw_sink < CLV_SINK_FULL || cfg->draw_sink > CLV_SINK_NONE) return fail(CLV_EINVAL, "bad draw_sink");
+  if (data->n < 0) return fail(CLV_EINVAL, "n must be >= 0");
+  if (cfg->n_global > 0xffffffffLL) return fail(CLV_EINVAL, "n_global must fit the 32-bit Philox customer counter");
+  if (cfg->n_global < data->n || cfg->n_global < 1) return fail(CLV_EINVAL, "n_global must be >= n >= 0 and > 0");
+  if (cfg->world_size < 1 || cfg->rank < 0 || cfg->rank >= cfg->world_size) return fail(CLV_EINVAL, "bad rank/world_size");
+  if (cfg->D == 3 && data->n > 0 && !data->log_s) return fail(CLV_EINVAL, "D == 3 needs log_s");
+  if (cfg->K > 1 && data->n > 0 && !data->covariates) return fail(CLV_EINVAL, "K > 1 needs covariates");
+  if (data->n > 0 && (!data->x || !data->t_x || !data->T_cal)) return fail(CLV_EINVAL, "missing CBS column");
+  if (cfg->rng_mode == CLV_RNG_REPLAY && cfg->world_size != 1) return fail(CLV_EINVAL, "replay needs world_size 1");
+
+  const int32_t bpu = cfg->blocks_per_unit ? cfg->blocks_per_unit : clv_default_blocks_per_unit(cfg->n_global);
+  if (!is_pow2(bpu)) return fail(CLV_EINVAL, "blocks_per_unit must be a power of two");
+  const int nb_local = (int)((data->n + BLOCK - 1) / BLOCK);
+  int32_t bpr = cfg->blocks_per_rank;
+  if (bpr == 0) {
+    if (cfg->world_size != 1) return fail(CLV_EINVAL, "blocks_per_rank required when sharded");
+    bpr = ((std::max(nb_local, 1) + bpu - 1) / bpu) * bpu;
+  }
+  if (bpr % bpu) return fail(CLV_EINVAL, "blocks_per_rank must be a multiple of blocks_per_unit");
+  if (nb_local > bpr) return fail(CLV_EINVAL, "shard larger than blocks_per_rank * CLV_BLOCK");
+  if (cfg->shard_begin != (int64_t)cfg->rank * bpr * BLOCK) return fail(CLV_EINVAL, "shard_begin != rank * blocks_per_rank * CLV_BLOCK");
+  const int64_t nb_global = (cfg->n_global + BLOCK - 1) / BLOCK;
+  if ((int64_t)bpr * cfg->world_size < nb_global) return fail(CLV_EINVAL, "shards do not cover n_global");
+
+  auto* s = new clv_sampler();
+  s->cfg = *cfg;
+  s->cfg.blocks_per_rank = bpr;
+  s->cfg.blocks_per_unit = bpu;
+  s->prior = *prior;
+  s->replay = cfg->rng_mode == CLV_RNG_REPLAY;
+
+  Geometry& g = s->g;
+  g.D = cfg->D;
+  g.K = cfg->K;
+  g.S = cfg->n_mh_steps;
+  g.n_chains = cfg->n_chains;
+  g.n = data->n;
+  g.n_global = cfg->n_global;
+  g.shard_begin = cfg->shard_begin;
+  g.nb_local = nb_local;
+  g.blocks_per_rank = bpr;
+  g.blocks_per_unit = bpu;
+  g.units_per_rank = bpr / bpu;
+  g.n_units_global = (nb_global + bpu - 1) / bpu;
+  g.world_size = cfg->world_size;
+  g.stride = cfg->K * cfg->D + cfg->D * (cfg->D + 1) / 2 + 1;
+  g.burnin = cfg->burnin;
+  g.mcmc = cfg->mcmc;
+  g.thin = cfg->thin;
+  g.n_draws = cfg->mcmc >= 1 ? (cfg->mcmc - 1) / cfg->thin + 1 : 0;
+  g.l2w = cfg->D * cfg->K + cfg->D * (cfg->D + 1) / 2;
+
+  auto cleanup_fail = [&](int rc) {
+    clv_destroy(s);
+    return rc;
+  };
+#define CLV_HIPC(expr)                                                                            \
+  do {                                                                                            \
+    hipError_t e_ = (expr);                                                                       \
+    if (e_ != hipSuccess)                                                                         \
+      return cleanup_fail(fail(CLV_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_)));    \
+  } while (0)
+
+  if (cfg->device >= 0) CLV_HIPC(hipSetDevice(cfg->device));
+  CLV_HIPC(hipGetDevice(&s->device));
+  if (cfg->stream) {
+    s->stream = (hipStream_t)(uintptr_t)cfg->stream;
+  } else {
+    CLV_HIPC(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+    s->own_stream = true;
+  }
+
+  const int64_t n = g.n, C = g.n_chains;
+  CLV_HIPC(dalloc(&s->d_x, std::max<int64_t>(n, 1)));
+  CLV_HIPC(dalloc(&s->d_tx, std::max<int64_t>(n, 1)));
+  CLV_HIPC(dalloc(&s->d_T, std::max<int64_t>(n, 1)));
+  if (g.K > 1) CLV_HIPC(dalloc(&s->d_cov, (size_t)(g.K - 1) * std::max<int64_t>(n, 1)));
+  if (g.D == 3) CLV_HIPC(dalloc(&s->d_logs, std::max<int64_t>(n, 1)));
+  CLV_HIPC(dalloc(&s->d_lam, C * std::max<int64_t>(n, 1)));
+  CLV_HIPC(dalloc(&s->d_mu, C * std::max<int64_t>(n, 1)));
+  CLV_HIPC(dalloc(&s->d_hyper, C * HS));
+  CLV_HIPC(dalloc(&s->d_block, (size_t)C * bpr * g.stride));
+  if (bpu > 1) CLV_HIPC(dalloc(&s->d_unit, (size_t)C * g.units_per_rank * g.stride));
+  else s->d_unit = s->d_block;
+  CLV_HIPC(dalloc(&s->d_prior, PRIOR_DOUBLES));
+  CLV_HIPC(dalloc(&s->d_ctrl, 1));
+  CLV_HIPC(dalloc(&s->d_bs, C * (CLV_MAX_K * CLV_MAX_D + CLV_MAX_D * CLV_MAX_D)));
+  if (g.n_draws > 0) {
+    CLV_HIPC(dalloc(&s->d_level2, (size_t)C * g.n_draws * g.l2w));
+    CLV_HIPC(dalloc(&s->d_loglik, (size_t)C * g.n_draws));
+    CLV_HIPC(hipMemsetAsync(s->d_level2, 0, sizeof(double) * C * g.n_draws * g.l2w, s->stream));
+    CLV_HIPC(hipMemsetAsync(s->d_loglik, 0, sizeof(double) * C * g.n_draws, s->stream));
+    if (cfg->draw_sink == CLV_SINK_FULL && n > 0) {
+      const size_t bytes = sizeof(double) * (size_t)C * g.n_draws * n * (g.D + 2);
+      CLV_HIPC(dalloc(&s->d_level1, bytes / sizeof(double)));
+      CLV_HIPC(hipMemsetAsync(s->d_level1, 0, bytes, s->stream));
+    }
+  }
+  if (cfg->draw_sink == CLV_SINK_SUMMARY && n > 0) {
+    CLV_HIPC(dalloc(&s->d_sums, (size_t)C * CLV_N_SUM_STATS * n));
+    CLV_HIPC(hipMemsetAsync(s->d_sums, 0, sizeof(double) * C * CLV_N_SUM_STATS * n, s->stream));
+  }
+  CLV_HIPC(hipMemsetAsync(s->d_block, 0, sizeof(double) * C * bpr * g.stride, s->stream));
+  if (bpu > 1) CLV_HIPC(hipMemsetAsync(s->d_unit, 0, sizeof(double) * C * g.units_per_rank * g.stride, s->stream));
+  CLV_HIPC(hipMemsetAsync(s->d_ctrl, 0, sizeof(Ctrl), s->stream));
+  CLV_HIPC(hipMemsetAsync(s->d_hyper, 0, sizeof(double) * C * HS, s->stream));
+
+  if (n > 0) {
+    CLV_HIPC(hipMemcpyAsync(s->d_x, data->x, sizeof(int32_t) * n, hipMemcpyHostToDevice, s->stream));
+    CLV_HIPC(hipMemcpyAsync(s->d_tx, data->t_x, sizeof(double) * n, hipMemcpyHostToDevice, s->stream));
+    CLV_HIPC(hipMemcpyAsync(s->d_T, data->T_cal, sizeof(double) * n, hipMemcpyHostToDevice, s->stream));
+    if (g.K > 1)
+      CLV_HIPC(hipMemcpyAsync(s->d_cov, data->covariates, sizeof(double) * (g.K - 1) * n, hipMemcpyHostToDevice, s->stream));
+    if (g.D == 3)
+      CLV_HIPC(hipMemcpyAsync(s->d_logs, data->log_s, sizeof(double) * n, hipMemcpyHostToDevice, s->stream));
+  }
+  {
+    std::vector<double> pr(PRIOR_DOUBLES, 0.0);
+    const int K = g.K, D = g.D;
+    for (int i = 0; i < K * K; ++i) {
+      pr[i] = prior->V[i];
+      pr[81 + i] = prior->chol_V[i];
+    }
+    for (int i = 0; i < K * D; ++i) pr[162 + i] = prior->A0B0[i];
+    for (int i = 0; i < D * D; ++i) pr[189 + i] = prior->S0_B0A0B0[i];
+    CLV_HIPC(hipMemcpyAsync(s->d_prior, pr.data(), sizeof(double) * PRIOR_DOUBLES, hipMemcpyHostToDevice, s->stream));
+    CLV_HIPC(hipStreamSynchronize(s->stream));
+  }
+
+  // Initial state (bi:367-379, tri:488-504) and, for D == 2, the statistics of the first draw.
+  if (n > 0) CLV_HIPC(launch_sweep(sweep_args(s, 1), false, s->stream));
+  else CLV_HIPC(hipMemsetAsync(s->d_block, 0, sizeof(double) * C * bpr * g.stride, s->stream));
+  if (bpu > 1) {
+    GroupArgs ga{};
+    ga.g = g;
+    ga.blockpart = s->d_block;
+    ga.unitpart = s->d_unit;
+    if (n > 0) CLV_HIPC(launch_group(ga, s->stream));
+  }
+  if (g.D == 3) {
+    std::vector<double> bs(C * (g.K * g.D + g.D * g.D));
+    for (int c = 0; c < C; ++c) {
+      double* o = bs.data() + c * (g.K * g.D + g.D * g.D);
+      for (int i = 0; i < g.K * g.D; ++i) o[i] = prior->beta_init[i];
+      for (int i = 0; i < g.D * g.D; ++i) o[g.K * g.D + i] = prior->sigma_init[i];
+    }
+    CLV_HIPC(hipMemcpyAsync(s->d_bs, bs.data(), sizeof(double) * bs.size(), hipMemcpyHostToDevice, s->stream));
+    CLV_HIPC(launch_set_hyper(g.D, g.K, (int)C, s->d_hyper, s->d_bs, prior->omega2, s->stream));
+  } else {
+    s->pending_init_hyper = true;
+  }
+  CLV_HIPC(hipStreamSynchronize(s->stream));
+#undef CLV_HIPC
+  *out = s;
+  return CLV_OK;
+}
+
+void clv_destroy(clv_sampler* s) {
+  if (!s) return;
+  (void)hipSetDevice(s->device);
+  if (s->stream) (void)hipStreamSynchronize(s->stream);
+  if (s->graph_exec) (void)hipGraphExecDestroy(s->graph_exec);
+  for (auto e : s->ev) (void)hipEventDestroy(e);
+  void* ptrs[] = {s->d_x, s->d_tx, s->d_T, s->d_cov, s->d_logs, s->d_lam, s->d_mu, s->d_hyper,
+                  s->d_block, s->d_prior, s->d_ctrl, s->d_level1, s->d_level2, s->d_loglik,
+                  s->d_sums, s->d_tape, s->d_bs};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  if (s->d_unit && s->d_unit != s->d_block) (void)hipFree(s->d_unit);
+  if (s->own_stream && s->stream) (void)hipStreamDestroy(s->stream);
+  delete s;
+}
+
+int clv_set_replay_tape(clv_sampler* s, const double* tape, int64_t n_sweeps) {
+  if (!s || !tape || n_sweeps < 1) return fail(CLV_EINVAL, "bad replay tape arguments");
+  if (!s->replay) return fail(CLV_ESTATE, "sampler not created in replay mode");
+  CLV_HIP(hipSetDevice(s->device));
+  if (s->d_tape) CLV_HIP(hipFree(s->d_tape));
+  s->d_tape = nullptr;
+  const size_t count = (size_t)s->g.n_chains * n_sweeps * clv_replay_sweep_stride(s);
+  CLV_HIP(dalloc(&s->d_tape, count));
+  CLV_HIP(hipMemcpy(s->d_tape, tape, count * sizeof(double), hipMemcpyHostToDevice));
+  s->tape_sweeps = n_sweeps;
+  if (s->graph_exec) {
+    CLV_HIP(hipGraphExecDestroy(s->graph_exec));
+    s->graph_exec = nullptr;
+  }
+  return CLV_OK;
+}
+
+int clv_hyper(clv_sampler* s, const double* gathered) {
+  if (!s) return fail(CLV_EINVAL, "null sampler");
+  if (s->g.world_size > 1 && !gathered) return fail(CLV_EINVAL, "sharded hyper needs the gathered buffer");
+  CLV_HIP(hipSetDevice(s->device));
+  if (s->pending_init_hyper) {
+    int rc = check_replay_range(s, 0);
+    if (rc) return rc;
+    rc = enqueue_hyper(s, gathered, 1, nullptr, nullptr);
+    if (rc) return rc;
+    s->pending_init_hyper = false;
+    return CLV_OK;
+  }
+  return enqueue_hyper(s, gathered, 0, nullptr, nullptr);
+}
+
+int clv_sweep(clv_sampler* s) {
+  if (!s) return fail(CLV_EINVAL, "null sampler");
+  if (s->pending_init_hyper) return fail(CLV_ESTATE, "bivariate: call clv_hyper once before the first sweep");
+  CLV_HIP(hipSetDevice(s->device));
+  int rc = check_replay_range(s, 1);
+  if (rc) return rc;
+  rc = enqueue_sweep(s, nullptr, nullptr);
+  if (rc) return rc;
+  s->sweeps_done++;
+  return CLV_OK;
+}
+
+int clv_partials(clv_sampler* s, double** ptr, int64_t* n_doubles, int32_t* stride) {
+  if (!s) return fail(CLV_EINVAL, "null sampler");
+  if (ptr) *ptr = s->d_unit;
+  if (n_doubles) *n_doubles = (int64_t)s->g.n_chains * s->g.units_per_rank * s->g.stride;
+  if (stride) *stride = s->g.stride;
+  return CLV_OK;
+}
+
+int clv_copy_partials(clv_sampler* s, void* dst) {
+  if (!s || !dst) return fail(CLV_EINVAL, "null argument");
+  CLV_HIP(hipSetDevice(s->device));
+  const size_t bytes = sizeof(double) * (size_t)s->g.n_chains * s->g.units_per_rank * s->g.stride;
+  CLV_HIP(hipMemcpyAsync(dst, s->d_unit, bytes, hipMemcpyDeviceToDevice, s->stream));
+  return CLV_OK;
+}
+
+int clv_synchronize(clv_sampler* s) {
+  if (!s) return fail(CLV_EINVAL, "null sampler");
+  CLV_HIP(hipSetDevice(s->device));
+  CLV_HIP(hipStreamSynchronize(s->stream));
+  return CLV_OK;
+}
+
+int64_t clv_sweeps_done(const clv_sampler* s) { return s ? s->sweeps_done : -1; }
+
+int clv_run(clv_sampler* s, int64_t n_sweeps) {
+  if (!s) return fail(CLV_EINVAL, "null sampler");
+  if (s->g.world_size != 1) return fail(CLV_ESTATE, "clv_run is unsharded; use clv_sweep/clv_hyper");
+  if (n_sweeps < 0) return fail(CLV_EINVAL, "n_sweeps < 0");
+  CLV_HIP(hipSetDevice(s->device));
+  int rc = check_replay_range(s, n_sweeps);
+  if (rc) return rc;
+  if (s->pending_init_hyper) {
+    rc = enqueue_hyper(s, nullptr, 1, nullptr, nullptr);
+    if (rc) return rc;
+    s->pending_init_hyper = false;
+  }
+  int64_t left = n_sweeps;
+  if (s->timing) {
+    if (s->ev.empty()) {
+      s->ev.resize(4 * TIMING_EVENTS);
+      for (auto& e : s->ev) CLV_HIP(hipEventCreate(&e));
+    }
+    while (left > 0) {
+      const int k = s->ev_used;
+      rc = enqueue_sweep(s, s->ev[4 * k], s->ev[4 * k + 1]);
+      if (rc == CLV_OK) rc = enqueue_hyper(s, nullptr, 0, s->ev[4 * k + 2], s->ev[4 * k + 3]);
+      if (rc) return rc;
+      s->ev_used++;
+      s->sweeps_done++;
+      left--;
+      if (s->ev_used == TIMING_EVENTS) {
+        rc = harvest_timing(s);
+        if (rc) return rc;
+      }
+    }
+    rc = harvest_timing(s);
+    if (rc) return rc;
+  } else {
+    if (left >= GRAPH_CHUNK) {
+      rc = build_graph(s, GRAPH_CHUNK);
+      if (rc) return rc;
+      while (left >= GRAPH_CHUNK) {
+        CLV_HIP(hipGraphLaunch(s->graph_exec, s->stream));
+        s->sweeps_done += GRAPH_CHUNK;
+        left -= GRAPH_CHUNK;
+      }
+    }
+    while (left > 0) {
+      rc = enqueue_sweep(s, nullptr, nullptr);
+      if (rc == CLV_OK) rc = enqueue_hyper(s, nullptr, 0, nullptr, nullptr);
+      if (rc) return rc;
+      s->sweeps_done++;
+      left--;
+    }
+  }
+  CLV_HIP(hipStreamSynchronize(s->stream));
+  return CLV_OK;
+}
+
+int clv_read_draws(clv_sampler* s, double* level1, double* level2, double* loglik) {
+  if (!s) return fail(CLV_EINVAL, "null sampler");
+  CLV_HIP(hipSetDevice(s->device));
+  CLV_HIP(hipStreamSynchronize(s->stream));
+  const Geometry& g = s->g;
+  const size_t C = g.n_chains;
+  if (level1) {
+    if (!s->d_level1 && g.n_draws > 0 && g.n > 0) return fail(CLV_ESTATE, "level-1 draws need draw_sink == CLV_SINK_FULL");
+    if (s->d_level1)
+      CLV_HIP(hipMemcpy(level1, s->d_level1, sizeof(double) * C * g.n_draws * g.n * (g.D + 2), hipMemcpyDeviceToHost));
+  }
+  if (level2 && s->d_level2)
+    CLV_HIP(hipMemcpy(level2, s->d_level2, sizeof(double) * C * g.n_draws * g.l2w, hipMemcpyDeviceToHost));
+  if (loglik && s->d_loglik)
+    CLV_HIP(hipMemcpy(loglik, s->d_loglik, sizeof(double) * C * g.n_draws, hipMemcpyDeviceToHost));
+  return CLV_OK;
+}
+
+int clv_read_summary(clv_sampler* s, double* sums, int64_t* n_stored) {
+  if (!s) return fail(CLV_EINVAL, "null sampler");
+  CLV_HIP(hipSetDevice(s->device));
+  CLV_HIP(hipStreamSynchronize(s->stream));
+  const Geometry& g = s->g;
+  if (n_stored) {
+    int64_t k = 0;
+    if (s->sweeps_done > g.burnin) k = (s->sweeps_done - 1 - g.burnin) / g.thin + 1;
+    *n_stored = std::min<int64_t>(k, g.n_draws);
+  }
+  if (sums) {
+    if (!s->d_sums) return fail(CLV_ESTATE, "summaries need draw_sink == CLV_SINK_SUMMARY");
+    CLV_HIP(hipMemcpy(sums, s->d_sums, sizeof(double) * g.n_chains * CLV_N_SUM_STATS * g.n, hipMemcpyDeviceToHost));
+  }
+  return CLV_OK;
+}
+
+int clv_get_state(clv_sampler* s, double* lambdas, double* mus, double* hyper) {
+  if (!s) return fail(CLV_EINVAL, "null sampler");
+  CLV_HIP(hipSetDevice(s->device));
+  CLV_HIP(hipStreamSynchronize(s->stream));
+  const Geometry& g = s->g;
+  if (lambdas && g.n) CLV_HIP(hipMemcpy(lambdas, s->d_lam, sizeof(double) * g.n_chains * g.n, hipMemcpyDeviceToHost));
+  if (mus && g.n) CLV_HIP(hipMemcpy(mus, s->d_mu, sizeof(double) * g.n_chains * g.n, hipMemcpyDeviceToHost));
+  if (hyper) {
+    std::vector<double> h((size_t)g.n_chains * HS);
+    CLV_HIP(hipMemcpy(h.data(), s->d_hyper, sizeof(double) * h.size(), hipMemcpyDeviceToHost));
+    const int w = g.K * g.D + g.D * g.D;
+    for (int c = 0; c < g.n_chains; ++c) {
+      for (int i = 0; i < g.K * g.D; ++i) hyper[c * w + i] = h[c * HS + H_BETA + i];
+      for (int p = 0; p < g.D; ++p)
+        for (int q = 0; q < g.D; ++q) hyper[c * w + g.K * g.D + p * g.D + q] = h[c * HS + H_SIGMA + p * 3 + q];
+    }
+  }
+  return CLV_OK;
+}
+
+int clv_set_state(clv_sampler* s, const double* lambdas, const double* mus, const double* hyper, int64_t sweeps_done) {
+  if (!s || sweeps_done < 0) return fail(CLV_EINVAL, "bad arguments");
+  CLV_HIP(hipSetDevice(s->device));
+  const Geometry& g = s->g;
+  if (lambdas && g.n) CLV_HIP(hipMemcpy(s->d_lam, lambdas, sizeof(double) * g.n_chains * g.n, hipMemcpyHostToDevice));
+  if (mus && g.n) CLV_HIP(hipMemcpy(s->d_mu, mus, sizeof(double) * g.n_chains * g.n, hipMemcpyHostToDevice));
+  if (hyper) {
+    CLV_HIP(hipMemcpy(s->d_bs, hyper, sizeof(double) * g.n_chains * (g.K * g.D + g.D * g.D), hipMemcpyHostToDevice));
+    CLV_HIP(launch_set_hyper(g.D, g.K, g.n_chains, s->d_hyper, s->d_bs, s->prior.omega2, s->stream));
+    s->pending_init_hyper = false;
+  }
+  Ctrl c{};
+  c.cur = sweeps_done;
+  CLV_HIP(hipMemcpyAsync(s->d_ctrl, &c, sizeof(Ctrl), hipMemcpyHostToDevice, s->stream));
+  CLV_HIP(hipStreamSynchronize(s->stream));
+  s->sweeps_done = sweeps_done;
+  return CLV_OK;
+}
+
+int clv_set_timing(clv_sampler* s, int32_t enable) {
+  if (!s) return fail(CLV_EINVAL, "null sampler");
+  s->timing = enable != 0;
+  s->t_sweep_ms = s->t_hyper_ms = 0.0;
+  s->n_sweep_timed = s->n_hyper_timed = 0;
+  return CLV_OK;
+}
+
+int clv_kernel_time(clv_sampler* s, double* sweep_ms, int64_t* n_sweep, double* hyper_ms, int64_t* n_hyper) {
+  if (!s) return fail(CLV_EINVAL, "null sampler");
+  if (sweep_ms) *sweep_ms = s->t_sweep_ms;
+  if (n_sweep) *n_sweep = s->n_sweep_timed;
+  if (hyper_ms) *hyper_ms = s->t_hyper_ms;
+  if (n_hyper) *n_hyper = s->n_hyper_timed;
+  return CLV_OK;
+}
+
+// ---- test hooks ----
+int clv_debug_philox(uint32_t k0, uint32_t k1, const uint32_t* ctr, int64_t n, uint32_t* out) {
+  if (!ctr || !out || n < 0) return fail(CLV_EINVAL, "bad arguments");
+  uint32_t *dc = nullptr, *dout = nullptr;
+  CLV_HIP(dalloc(&dc, 4 * std::max<int64_t>(n, 1)));
+  CLV_HIP(dalloc(&dout, 4 * std::max<int64_t>(n, 1)));
+  CLV_HIP(hipMemcpy(dc, ctr, 16 * n, hipMemcpyHostToDevice));
+  CLV_HIP(launch_debug_philox(k0, k1, dc, n, dout, nullptr));
+  CLV_HIP(hipMemcpy(out, dout, 16 * n, hipMemcpyDeviceToHost));
+  CLV_HIP(hipFree(dc));
+  CLV_HIP(hipFree(dout));
+  return CLV_OK;
+}
+
+int clv_debug_variates(uint64_t seed, int32_t chain, uint32_t sweep, int64_t n, int32_t S, float* tl, float* tm,
+                       float* ua, double* uz, double* ut, double* ea, double* ez) {
+  if (n < 1 || S < 0) return fail(CLV_EINVAL, "bad arguments");
+  const int64_t nS = std::max<int64_t>(n * S, 1);
+  float *dtl, *dtm, *dua;
+  double *duz, *dut, *dea, *dez;
+  CLV_HIP(dalloc(&dtl, nS));
+  CLV_HIP(dalloc(&dtm, nS));
+  CLV_HIP(dalloc(&dua, nS));
+  CLV_HIP(dalloc(&duz, n));
+  CLV_HIP(dalloc(&dut, n));
+  CLV_HIP(dalloc(&dea, n));
+  CLV_HIP(dalloc(&dez, n));
+  CLV_HIP(launch_debug_variates(seed, chain, sweep, n, S, dtl, dtm, dua, duz, dut, dea, dez, nullptr));
+  if (S > 0) {
+    CLV_HIP(hipMemcpy(tl, dtl, sizeof(float) * n * S, hipMemcpyDeviceToHost));
+    CLV_HIP(hipMemcpy(tm, dtm, sizeof(float) * n * S, hipMemcpyDeviceToHost));
+    CLV_HIP(hipMemcpy(ua, dua, sizeof(float) * n * S, hipMemcpyDeviceToHost));
+  }
+  CLV_HIP(hipMemcpy(uz, duz, sizeof(double) * n, hipMemcpyDeviceToHost));
+  CLV_HIP(hipMemcpy(ut, dut, sizeof(double) * n, hipMemcpyDeviceToHost));
+  CLV_HIP(hipMemcpy(ea, dea, sizeof(double) * n, hipMemcpyDeviceToHost));
+  CLV_HIP(hipMemcpy(ez, dez, sizeof(double) * n, hipMemcpyDeviceToHost));
+  for (void* p : {(void*)dtl, (void*)dtm, (void*)dua, (void*)duz, (void*)dut, (void*)dea, (void*)dez})
+    CLV_HIP(hipFree(p));
+  return CLV_OK;
+}
+
+int clv_debug_level2(int32_t D, int32_t K, const clv_prior* prior, const double* xty, const double* yty,
+                     const double* iwn, const double* chi2, const double* z, double* beta, double* sigma) {
+  if ((D != 2 && D != 3) || K < 1 || K > CLV_MAX_K || !prior) return fail(CLV_EINVAL, "bad arguments");
+  std::vector<double> pr(PRIOR_DOUBLES, 0.0);
+  for (int i = 0; i < K * K; ++i) {
+    pr[i] = prior->V[i];
+    pr[81 + i] = prior->chol_V[i];
+  }
+  for (int i = 0; i < K * D; ++i) pr[162 + i] = prior->A0B0[i];
+  for (int i = 0; i < D * D; ++i) pr[189 + i] = prior->S0_B0A0B0[i];
+  std::vector<double> in(K * D + D * D + 6 + D * K, 0.0);
+  for (int i = 0; i < K * D; ++i) in[i] = xty[i];
+  for (int i = 0; i < D * D; ++i) in[K * D + i] = yty[i];
+  for (int i = 0; i < D * (D - 1) / 2; ++i) in[K * D + D * D + i] = iwn[i];
+  for (int i = 0; i < D; ++i) in[K * D + D * D + 3 + i] = chi2[i];
+  for (int i = 0; i < D * K; ++i) in[K * D + D * D + 6 + i] = z[i];
+  double *dpr, *din, *dout;
+  CLV_HIP(dalloc(&dpr, pr.size()));
+  CLV_HIP(dalloc(&din, in.size()));
+  CLV_HIP(dalloc(&dout, K * D + D * D));
+  CLV_HIP(hipMemcpy(dpr, pr.data(), sizeof(double) * pr.size(), hipMemcpyHostToDevice));
+  CLV_HIP(hipMemcpy(din, in.data(), sizeof(double) * in.size(), hipMemcpyHostToDevice));
+  CLV_HIP(launch_debug_level2(D, K, dpr, din, dout, nullptr));
+  std::vector<double> o(K * D + D * D);
+  CLV_HIP(hipMemcpy(o.data(), dout, sizeof(double) * o.size(), hipMemcpyDeviceToHost));
+  for (int i = 0; i < K * D; ++i) beta[i] = o[i];
+  for (int i = 0; i < D * D; ++i) sigma[i] = o[K * D + i];
+  CLV_HIP(hipFree(dpr));
+  CLV_HIP(hipFree(din));
+  CLV_HIP(hipFree(dout));
+  return CLV_OK;
+}
+
+int clv_debug_hyper_variates(uint64_t seed, int32_t chain, uint32_t sweep, double df, int64_t n, double* chi2,
+                             double* normals) {
+  if (n < 1 || df < 2.0) return fail(CLV_EINVAL, "bad arguments");
+  double *dc, *dn;
+  CLV_HIP(dalloc(&dc, n));
+  CLV_HIP(dalloc(&dn, n));
+  CLV_HIP(launch_debug_hyper_variates(seed, chain, sweep, df, n, dc, dn, nullptr));
+  CLV_HIP(hipMemcpy(chi2, dc, sizeof(double) * n, hipMemcpyDeviceToHost));
+  CLV_HIP(hipMemcpy(normals, dn, sizeof(double) * n, hipMemcpyDeviceToHost));
+  CLV_HIP(hipFree(dc));
+  CLV_HIP(hipFree(dn));
+  return CLV_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,113 @@
+// Shared declarations between the HIP kernels (kernels.hip) and the C ABI (capi.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/clvmcmc.h"
+
+namespace clv {
+
+constexpr int BLOCK = CLV_BLOCK;       // customers (lanes) per sweep workgroup
+constexpr int HS = 64;                 // doubles of hyper state per chain
+constexpr int TAPE_HYPER = 40;         // doubles of hyper variates per recorded sweep
+
+// Hyper-state layout (per chain, HS doubles).
+enum : int {
+  H_BETA = 0,        // K x D row-major, beta[k][d] at k*D + d   (<= 27)
+  H_SIGMA = 27,      // 3 x 3 row-major (D x D used)
+  H_P00 = 36, H_P01 = 37, H_P11 = 38,  // inv(Sigma)[0:2,0:2] (bi:283, tri:402 quirk Q4)
+  H_S00 = 39, H_S11 = 40,              // proposal scales Sigma[0,0], Sigma[1,1] (quirk Q2)
+  H_S22 = 41, H_POSTVAR = 42, H_SQRT_POSTVAR = 43, H_OMEGA2 = 44,  // draw_eta (tri:321-333)
+};
+
+struct Ctrl {
+  int64_t cur;        // sweeps completed; the next sweep kernel runs sweep cur + 1
+  uint32_t arrive;    // arrival counter of the hyper kernel's workgroups
+  uint32_t pad;
+};
+
+struct Geometry {
+  int D, K, S;               // S = n_mh_steps
+  int n_chains;
+  int64_t n;                 // local customers
+  int64_t n_global;
+  int64_t shard_begin;
+  int nb_local;              // ceil(n / BLOCK)
+  int blocks_per_rank;
+  int blocks_per_unit;       // G_b: blocks summed into one exchanged unit (power of two)
+  int units_per_rank;
+  int64_t n_units_global;
+  int world_size;
+  int stride;                // doubles per partial: K*D + D(D+1)/2 + 1
+  int burnin, mcmc, thin, n_draws;
+  int l2w;                   // level-2 record width: D*K + D(D+1)/2
+};
+
+struct Rng {
+  uint64_t seed;
+  int chain_first;
+  const double* tape;        // replay tape (device), [chain][sweep][tape_sweep_stride]
+  int64_t tape_sweep_stride;
+  int64_t tape_sweeps;
+};
+
+struct SweepArgs {
+  Geometry g;
+  Rng r;
+  const int32_t* x;
+  const double* tx;
+  const double* T;
+  const double* cov;         // (K-1) x n
+  const double* log_s;
+  double* lam;               // [chain][n]
+  double* mu;
+  const double* hyper;       // [chain][HS]
+  double* blockpart;         // [chain][blocks_per_rank][stride]
+  const Ctrl* ctrl;
+  double* level1;            // [chain][n_draws][n][D+2] or null
+  double* sums;              // [chain][CLV_N_SUM_STATS][n] or null
+  int64_t* n_stored;         // device counter of stored draws (chain 0 block 0 bumps it)
+  double lam_init;
+  int init;                  // 1: initialisation pass (bi:367-370), no sweep
+};
+
+struct GroupArgs {
+  Geometry g;
+  const double* blockpart;
+  double* unitpart;          // [chain][units_per_rank][stride]
+};
+
+struct HyperArgs {
+  Geometry g;
+  Rng r;
+  const double* units;       // [world][chain][units_per_rank][stride]
+  double* hyper;             // [chain][HS]
+  Ctrl* ctrl;
+  double* level2;            // [chain][n_draws][l2w]
+  double* loglik;            // [chain][n_draws]
+  const double* V;           // K x K
+  const double* cholV;       // K x K lower
+  const double* A0B0;        // K x D
+  const double* S0B;         // D x D: S0 + B0'A0B0
+  double nu_n;
+  double omega2;
+  int mode;                  // 0: after sweep (cur+1); 1: bivariate initial draw (sweep 1)
+};
+
+// Launchers (kernels.hip).
+hipError_t launch_sweep(const SweepArgs& a, bool replay, hipStream_t st);
+hipError_t launch_group(const GroupArgs& a, hipStream_t st);
+hipError_t launch_hyper(const HyperArgs& a, bool replay, hipStream_t st);
+hipError_t launch_set_hyper(int D, int K, int n_chains, double* hyper, const double* beta_sigma,
+                            double omega2, hipStream_t st);
+hipError_t launch_debug_philox(uint32_t k0, uint32_t k1, const uint32_t* ctr, int64_t n, uint32_t* out,
+                               hipStream_t st);
+hipError_t launch_debug_variates(uint64_t seed, int chain, uint32_t sweep, int64_t n, int S, float* tl,
+                                 float* tm, float* ua, double* uz, double* ut, double* ea, double* ez,
+                                 hipStream_t st);
+hipError_t launch_debug_level2(int D, int K, const double* prior_dev, const double* in, double* out,
+                               hipStream_t st);
+hipError_t launch_debug_hyper_variates(uint64_t seed, int chain, uint32_t sweep, double df, int64_t n,
+                                       double* chi2, double* normals, hipStream_t st);
+
+}  // namespace clv

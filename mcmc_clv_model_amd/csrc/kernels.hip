@@ -1,0 +1,736 @@
+// HIP kernels of the MI355X-native Abe (2009/2015) HB Pareto/NBD sampler (gfx950).
+//
+//   sweep_kernel  one lane per (chain, customer): draw_z, draw_tau, the n_mh_steps MH updates of
+//                 (log lambda, log mu), draw_eta (D == 3), draw storage, and the customer's
+//                 contribution to the level-2 sufficient statistics X'Y, Y'Y (+ log-lik term),
+//                 reduced to one partial per workgroup of CLV_BLOCK customers.
+//   group_kernel  sums blocks_per_unit consecutive block partials (large N: fewer exchanged units).
+//   hyper_kernel  one workgroup per chain: fixed-order sum of all unit partials, then the
+//                 conjugate multivariate-regression / inverse-Wishart draw (bi:233-262).
+//
+// Reference: src/models/bivariate/mcmc.py (bi), src/models/trivariate/mcmc.py (tri).
+// All model arithmetic is float64 and follows the reference's operation order, so that with
+// replayed variates (CLV_RNG_REPLAY) trajectories agree with the reference to rounding.
+#include "kernels.h"
+#include "philox.h"
+
+namespace clv {
+
+__device__ __forceinline__ double clip70(double v) {  // np.clip(v, -70, 70), NaN passes (bi:323)
+  return v < -70.0 ? -70.0 : (v > 70.0 ? 70.0 : v);
+}
+__device__ __forceinline__ double min700(double v) {  // np.minimum(700, v) (bi:223)
+  return v > 700.0 ? 700.0 : v;
+}
+
+// Per-customer constants of log_posterior (bi:291-310).
+struct LPConst {
+  double xm, omz, w, m0, m1, p00, p01, p11;
+};
+
+__device__ __forceinline__ double log_post(const LPConst& c, double ll, double lm) {
+  const double dl = ll - c.m0;
+  const double dm = lm - c.m1;
+  const double lik = (c.xm * ll + c.omz * lm) - (exp(ll) + exp(lm)) * c.w;
+  const double prior = -0.5 * ((dl * dl * c.p00 + 2.0 * dl * dm * c.p01) + dm * dm * c.p11);
+  const double res = lik + prior;
+  return lm > 5.0 ? -__builtin_inf() : res;  // cap (quirk Q3)
+}
+
+// Deterministic workgroup reduction of NS doubles (fixed butterfly + fixed wave order).
+// Result valid in `out` (LDS) for all threads after the call.
+template <int NS>
+__device__ __forceinline__ void block_reduce(double (&v)[NS], double (*red)[NS], double* out) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  constexpr int NW = BLOCK / 64;
+#pragma unroll
+  for (int j = 0; j < NS; ++j) {
+    double t = v[j];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) t += __shfl_xor(t, off, 64);
+    v[j] = t;
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int j = 0; j < NS; ++j) red[wave][j] = v[j];
+  }
+  __syncthreads();
+  if (threadIdx.x < NS) {
+    double t = red[0][threadIdx.x];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) t += red[w][threadIdx.x];
+    out[threadIdx.x] = t;
+  }
+  __syncthreads();
+}
+
+// bi:402 (the reference's loop ends at burnin + mcmc, bi:383, so nothing beyond is stored)
+__device__ __forceinline__ bool is_stored(int64_t s, const Geometry& g) {
+  return s > g.burnin && s <= (int64_t)g.burnin + g.mcmc && ((s - 1 - g.burnin) % g.thin) == 0;
+}
+__device__ __forceinline__ int64_t draw_index(int64_t s, const Geometry& g) {
+  return (s - 1 - g.burnin) / g.thin;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Sweep kernel
+// ---------------------------------------------------------------------------------------------
+template <int D, int K, bool REPLAY>
+__global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
+  constexpr int NXY = K * D;
+  constexpr int NYY = D * (D + 1) / 2;
+  constexpr int NS = NXY + NYY + 1;
+  __shared__ double red[BLOCK / 64][NS];
+  __shared__ double tot[NS];
+
+  const Geometry& g = a.g;
+  const int c = blockIdx.y;
+  const int b = blockIdx.x;
+  const int64_t i = (int64_t)b * BLOCK + threadIdx.x;
+  const bool active = i < g.n;
+  const int64_t s = a.init ? 0 : __hip_atomic_load(&a.ctrl->cur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  const bool stored = !a.init && is_stored(s, g);
+
+  double acc[NS];
+#pragma unroll
+  for (int j = 0; j < NS; ++j) acc[j] = 0.0;
+
+  if (active) {
+    const double* H = a.hyper + (int64_t)c * HS;
+    const int64_t ci = (int64_t)c * g.n + i;
+    const double tx = a.tx[i];
+    const double T = a.T[i];
+    double xr[K];
+    xr[0] = 1.0;
+#pragma unroll
+    for (int k = 1; k < K; ++k) xr[k] = a.cov[(int64_t)(k - 1) * g.n + i];
+
+    double lam, mu, eta = 1.0, Y[D];
+    if (a.init) {
+      // bi:368-370 / tri:489-491
+      lam = a.lam_init;
+      mu = 1.0 / (tx + 0.5 / a.lam_init);
+      Y[0] = log(lam);
+      Y[1] = log(mu);
+      if constexpr (D == 3) Y[2] = 0.0;
+    } else {
+      lam = a.lam[ci];
+      mu = a.mu[ci];
+      const double xm = (double)a.x[i];
+      uint32_t k0 = 0, k1 = 0;
+      const double* tape = nullptr;
+      if constexpr (REPLAY) {
+        tape = a.r.tape + ((int64_t)c * a.r.tape_sweeps + (s - 1)) * a.r.tape_sweep_stride;
+      } else {
+        chain_key(a.r.seed, (int64_t)a.r.chain_first + c, &k0, &k1);
+      }
+      const uint32_t gi = (uint32_t)(g.shard_begin + i);
+
+      // ---- draw_z (bi:193-200)
+      // Replay: u_z and the per-customer tau variate (standard exponential if alive, uniform if
+      // churned — the reference's consumption order, bi:215-225). Philox: slot SLOT_ZTAU words
+      // (x, y) -> u_z, (z, w) -> U in [0,1) for churned / -log(U') with U' in (0,1] for alive.
+      double u_z;
+      uint32_t rz = 0, rw = 0;
+      double v_tau = 0.0;
+      if constexpr (REPLAY) {
+        u_z = tape[i];
+        v_tau = tape[g.n + i];
+      } else {
+        const u32x4 r = customer_block(k0, k1, gi, (uint32_t)s, SLOT_ZTAU);
+        u_z = u53(r.x, r.y);
+        rz = r.z;
+        rw = r.w;
+      }
+      const double ml = mu + lam;
+      const double zz = ml * (T - tx);
+      const double e = exp(-zz);
+      const double p = (ml * e) / (ml * e + mu * (1.0 - e));
+      const bool z = u_z < p;
+
+      // ---- draw_tau (bi:203-227)
+      double tau;
+      if (z) {
+        double E;
+        if constexpr (REPLAY) E = v_tau; else E = -log(u53_open0(rz, rw));
+        tau = T + (1.0 / mu) * E;
+      } else {
+        double u;
+        if constexpr (REPLAY) u = v_tau; else u = u53(rz, rw);
+        const double ml_tx = min700(ml * tx);
+        const double ml_T = min700(ml * T);
+        tau = -log((1 - u) * exp(-ml_tx) + u * exp(-ml_T)) / ml;
+      }
+
+      // ---- _draw_level_1 (bi:268-339): mv_mean = X @ beta (bi:284)
+      double m0 = 0.0, m1 = 0.0;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        m0 += xr[k] * H[H_BETA + k * D + 0];
+        m1 += xr[k] * H[H_BETA + k * D + 1];
+      }
+      LPConst lc;
+      lc.xm = xm;
+      lc.omz = z ? 0.0 : 1.0;
+      lc.w = z ? T : tau;
+      lc.m0 = m0;
+      lc.m1 = m1;
+      lc.p00 = H[H_P00];
+      lc.p01 = H[H_P01];
+      lc.p11 = H[H_P11];
+      const double s00 = H[H_S00];
+      const double s11 = H[H_S11];
+      double ll = log(lam);
+      double lm = log(mu);
+      double cur = log_post(lc, ll, lm);
+      for (int j = 0; j < g.S; ++j) {
+        double pl, pm, plp;
+        bool accept;
+        if constexpr (REPLAY) {
+          const double tl = tape[(int64_t)(2 + 3 * j) * g.n + i];
+          const double tm = tape[(int64_t)(3 + 3 * j) * g.n + i];
+          const double u = tape[(int64_t)(4 + 3 * j) * g.n + i];
+          pl = clip70(ll + s00 * tl);
+          pm = clip70(lm + s11 * tm);
+          plp = log_post(lc, pl, pm);
+          accept = exp(plp - cur) > u;           // bi:329-330
+        } else {
+          const u32x4 ra = customer_block(k0, k1, gi, (uint32_t)s, SLOT_MH0 + 2u * j);
+          const u32x4 rb = customer_block(k0, k1, gi, (uint32_t)s, SLOT_MH0 + 2u * j + 1u);
+          float tl, tm, lu;
+          mh_variates(ra, rb, &tl, &tm, &lu);
+          pl = clip70(ll + s00 * (double)tl);
+          pm = clip70(lm + s11 * (double)tm);
+          plp = log_post(lc, pl, pm);
+          accept = (plp - cur) > (double)lu;     // exp(d) > u  <=>  d > log(u)
+        }
+        if (accept) {
+          ll = pl;
+          lm = pm;
+          cur = plp;
+        }
+      }
+      lam = exp(ll);  // bi:337-338
+      mu = exp(lm);
+
+      // ---- draw_eta (tri:306-333, call site tri:524-526)
+      if constexpr (D == 3) {
+        double m2 = 0.0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) m2 += xr[k] * H[H_BETA + k * D + 2];
+        const double post_var = H[H_POSTVAR];
+        const double post_mean = post_var * (a.log_s[i] / H[H_OMEGA2] + m2 / H[H_S22]);
+        double zeta;
+        if constexpr (REPLAY) {
+          zeta = tape[(int64_t)(2 + 3 * g.S) * g.n + i];
+        } else {
+          const u32x4 r = customer_block(k0, k1, gi, (uint32_t)s, SLOT_ETA);
+          zeta = sqrt(-2.0 * log(u53_open0(r.x, r.y))) * cospi(2.0 * u53(r.z, r.w));
+        }
+        eta = exp(post_mean + H[H_SQRT_POSTVAR] * zeta);
+        // tri: level 2 sees log(lambda) before the storage round trip (tri:529-536 before :542)
+        Y[0] = log(lam);
+        Y[1] = log(mu);
+        Y[2] = log(eta);
+      }
+
+      // ---- storage (bi:402-428, tri:539-571)
+      if (stored) {
+        lam = exp(log(lam));  // quirk Q5 (bi:405-406)
+        mu = exp(log(mu));
+        const int64_t dr = draw_index(s, g);
+        if (a.level1) {
+          double* o = a.level1 + (((int64_t)c * g.n_draws + dr) * g.n + i) * (D + 2);
+          o[0] = lam;
+          o[1] = mu;
+          o[2] = tau;
+          o[3] = z ? 1.0 : 0.0;
+          if constexpr (D == 3) o[4] = eta;
+        }
+        const double lgl = log(lam), lgm = log(mu);
+        acc[NS - 1] = (xm * lgl + lc.omz * lgm) - (lam + mu) * lc.w;  // bi:423-427
+        if (a.sums) {
+          double* sm = a.sums + (int64_t)c * CLV_N_SUM_STATS * g.n + i;
+          sm[CLV_SUM_LAMBDA * g.n] += lam;
+          sm[CLV_SUM_MU * g.n] += mu;
+          sm[CLV_SUM_Z * g.n] += z ? 1.0 : 0.0;
+          sm[CLV_SUM_LOG_LAMBDA * g.n] += lgl;
+          sm[CLV_SUM_LOG_MU * g.n] += lgm;
+          sm[CLV_SUM_LAMBDA2 * g.n] += lam * lam;
+          sm[CLV_SUM_MU2 * g.n] += mu * mu;
+          if constexpr (D == 3) {
+            sm[CLV_SUM_ETA * g.n] += eta;
+            sm[CLV_SUM_LOG_ETA * g.n] += log(eta);
+          }
+        }
+      }
+      if constexpr (D == 2) {
+        // bi: the next level-2 draw uses log of the carried state (bi:393)
+        Y[0] = log(lam);
+        Y[1] = log(mu);
+      }
+    }
+    a.lam[ci] = lam;
+    a.mu[ci] = mu;
+
+    // ---- sufficient statistics: X'Y (K x D) and Y'Y (upper triangle)
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+#pragma unroll
+      for (int d = 0; d < D; ++d) acc[k * D + d] = xr[k] * Y[d];
+    int t = NXY;
+#pragma unroll
+    for (int p = 0; p < D; ++p)
+#pragma unroll
+      for (int q = p; q < D; ++q) acc[t++] = Y[p] * Y[q];
+  }
+
+  block_reduce<NS>(acc, red, tot);
+  if (threadIdx.x < NS)
+    a.blockpart[((int64_t)c * g.blocks_per_rank + b) * g.stride + threadIdx.x] = tot[threadIdx.x];
+}
+
+// ---------------------------------------------------------------------------------------------
+// Group kernel: unit partial = sequential sum of blocks_per_unit block partials.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void group_kernel(GroupArgs a) {
+  const Geometry& g = a.g;
+  const int u = blockIdx.x;
+  const int c = blockIdx.y;
+  const int j = threadIdx.x;
+  if (j >= g.stride) return;
+  const double* p = a.blockpart + ((int64_t)c * g.blocks_per_rank + (int64_t)u * g.blocks_per_unit) * g.stride + j;
+  double t = 0.0;
+  for (int bb = 0; bb < g.blocks_per_unit; ++bb) t += p[(int64_t)bb * g.stride];
+  a.unitpart[((int64_t)c * g.units_per_rank + u) * g.stride + j] = t;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Level-2 algebra (bi:243-261) on reduced statistics.
+// ---------------------------------------------------------------------------------------------
+template <int D>
+__device__ void cholesky(const double (&A)[D][D], double (&L)[D][D]) {
+#pragma unroll
+  for (int r = 0; r < D; ++r)
+#pragma unroll
+    for (int q = 0; q < D; ++q) L[r][q] = 0.0;
+#pragma unroll
+  for (int j = 0; j < D; ++j) {
+    double sdiag = A[j][j];
+#pragma unroll
+    for (int k = 0; k < j; ++k) sdiag -= L[j][k] * L[j][k];
+    L[j][j] = sqrt(sdiag);
+#pragma unroll
+    for (int r = j + 1; r < D; ++r) {
+      double sv = A[r][j];
+#pragma unroll
+      for (int k = 0; k < j; ++k) sv -= L[r][k] * L[j][k];
+      L[r][j] = sv / L[j][j];
+    }
+  }
+}
+
+// hyper-state finalisation from (beta, Sigma): inverse block, proposal scales, eta constants.
+template <int D, int K>
+__device__ void finalize_hyper(const double (&beta)[K][D], const double (&Sig)[D][D], double omega2, double* H) {
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+#pragma unroll
+    for (int d = 0; d < D; ++d) H[H_BETA + k * D + d] = beta[k][d];
+  for (int q = 0; q < 9; ++q) H[H_SIGMA + q] = 0.0;
+#pragma unroll
+  for (int p = 0; p < D; ++p)
+#pragma unroll
+    for (int q = 0; q < D; ++q) H[H_SIGMA + p * 3 + q] = Sig[p][q];
+  if constexpr (D == 2) {
+    const double det = Sig[0][0] * Sig[1][1] - Sig[0][1] * Sig[1][0];
+    H[H_P00] = Sig[1][1] / det;
+    H[H_P01] = -Sig[0][1] / det;
+    H[H_P11] = Sig[0][0] / det;
+  } else {
+    // top-left 2x2 block of the full 3x3 inverse (tri:402 with tri:422-424; quirk Q4)
+    const double c00 = Sig[1][1] * Sig[2][2] - Sig[1][2] * Sig[2][1];
+    const double c01 = Sig[1][0] * Sig[2][2] - Sig[1][2] * Sig[2][0];
+    const double c02 = Sig[1][0] * Sig[2][1] - Sig[1][1] * Sig[2][0];
+    const double det = Sig[0][0] * c00 - Sig[0][1] * c01 + Sig[0][2] * c02;
+    H[H_P00] = c00 / det;
+    H[H_P01] = -(Sig[0][1] * Sig[2][2] - Sig[0][2] * Sig[2][1]) / det;
+    H[H_P11] = (Sig[0][0] * Sig[2][2] - Sig[0][2] * Sig[2][0]) / det;
+    H[H_S22] = Sig[2][2];
+    const double post_var = 1.0 / (1.0 / omega2 + 1.0 / Sig[2][2]);  // tri:325-326
+    H[H_POSTVAR] = post_var;
+    H[H_SQRT_POSTVAR] = sqrt(post_var);
+    H[H_OMEGA2] = omega2;
+  }
+  H[H_S00] = Sig[0][0];
+  H[H_S11] = Sig[1][1];
+}
+
+// Given the reduced statistics and the variates, draw (beta, Sigma).
+// iwn: n_tril normals, chi2: D chi-square draws, noise: either the replayed mvn noise (w, D*K) or
+// standard normals z (D*K) mapped through kron(chol(Sigma), chol(V)).
+template <int D, int K>
+__device__ void level2_draw(const double* tot, const double* V, const double* cholV, const double* A0B0,
+                            const double* S0B, const double* iwn, const double* chi2, const double* noise,
+                            bool noise_is_w, double (&beta)[K][D], double (&Sig)[D][D]) {
+  constexpr int NXY = K * D;
+  double R[K][D], Bh[K][D];
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+#pragma unroll
+    for (int d = 0; d < D; ++d) R[k][d] = tot[k * D + d] + A0B0[k * D + d];
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      double sv = 0.0;
+#pragma unroll
+      for (int j = 0; j < K; ++j) sv += V[k * K + j] * R[j][d];
+      Bh[k][d] = sv;
+    }
+  // S_n = S0 + Y'Y + B0'A0B0 - R'B_hat   (== S0 + E'E + C'A0C, bi:253-255)
+  double Sn[D][D];
+  int t = NXY;
+#pragma unroll
+  for (int p = 0; p < D; ++p)
+#pragma unroll
+    for (int q = p; q < D; ++q) {
+      double rb = 0.0;
+#pragma unroll
+      for (int k = 0; k < K; ++k) rb += R[k][p] * Bh[k][q];
+      const double v = (S0B[p * D + q] + tot[t++]) - rb;
+      Sn[p][q] = v;
+      Sn[q][p] = v;
+    }
+  // Sigma ~ IW(nu_n, S_n): scipy invwishart Bartlett form, Sigma = (L A^-1)(L A^-1)'
+  double L[D][D], A[D][D], M[D][D];
+  cholesky<D>(Sn, L);
+#pragma unroll
+  for (int p = 0; p < D; ++p)
+#pragma unroll
+    for (int q = 0; q < D; ++q) A[p][q] = 0.0;
+  {
+    int n = 0;
+#pragma unroll
+    for (int p = 1; p < D; ++p)
+#pragma unroll
+      for (int q = 0; q < p; ++q) A[p][q] = iwn[n++];  // np.tril_indices(D, -1) order
+#pragma unroll
+    for (int p = 0; p < D; ++p) A[p][p] = sqrt(chi2[p]);
+  }
+#pragma unroll
+  for (int r = 0; r < D; ++r)
+#pragma unroll
+    for (int j = D - 1; j >= 0; --j) {
+      double sv = L[r][j];
+#pragma unroll
+      for (int k = j + 1; k < D; ++k) sv -= M[r][k] * A[k][j];
+      M[r][j] = sv / A[j][j];
+    }
+#pragma unroll
+  for (int p = 0; p < D; ++p)
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+      double sv = 0.0;
+#pragma unroll
+      for (int k = 0; k < D; ++k) sv += M[p][k] * M[q][k];
+      Sig[p][q] = sv;
+    }
+#pragma unroll
+  for (int p = 0; p < D; ++p)
+#pragma unroll
+    for (int q = p + 1; q < D; ++q) Sig[q][p] = Sig[p][q];
+  // beta | Sigma: MVN(B_hat.ravel(), kron(Sigma, V)) with the reference's row-major ravel (quirk Q1)
+  double w[D * K];
+  if (noise_is_w) {
+#pragma unroll
+    for (int q = 0; q < D * K; ++q) w[q] = noise[q];
+  } else {
+    double Ls[D][D];
+    cholesky<D>(Sig, Ls);
+#pragma unroll
+    for (int p = 0; p < D; ++p)
+#pragma unroll
+      for (int bq = 0; bq < K; ++bq) {
+        double sv = 0.0;
+#pragma unroll
+        for (int cc = 0; cc <= p; ++cc)
+#pragma unroll
+          for (int e = 0; e <= bq; ++e) sv += Ls[p][cc] * cholV[bq * K + e] * noise[cc * K + e];
+        w[p * K + bq] = sv;
+      }
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+#pragma unroll
+    for (int d = 0; d < D; ++d) beta[k][d] = Bh[k][d] + w[k * D + d];
+}
+
+// Philox-mode hyper variates (fp64).
+__device__ double hyper_normal(uint32_t k0, uint32_t k1, uint32_t slot, uint32_t sweep) {
+  const u32x4 r = hyper_block(k0, k1, slot, sweep);
+  return sqrt(-2.0 * log(u53_open0(r.x, r.y))) * cospi(2.0 * u53(r.z, r.w));
+}
+
+// Marsaglia–Tsang Gamma(alpha, 1), alpha >= 1; chi2(df) = 2 Gamma(df / 2).
+__device__ double chi2_draw(uint32_t k0, uint32_t k1, uint32_t sweep, int idx, double df) {
+  const double alpha = 0.5 * df;
+  const double dd = alpha - 1.0 / 3.0;
+  const double cc = 1.0 / sqrt(9.0 * dd);
+  for (int at = 0; at < GAMMA_MAX_ATTEMPTS; ++at) {
+    const uint32_t slot = HSLOT_GAMMA0 + (uint32_t)idx * HSLOT_GAMMA_STRIDE + 2u * at;
+    const double x = hyper_normal(k0, k1, slot, sweep);
+    const double t = cc * x;
+    if (t <= -1.0) continue;
+    const double v1 = t * (3.0 + t * (3.0 + t));  // (1 + t)^3 - 1
+    const u32x4 r2 = hyper_block(k0, k1, slot + 1u, sweep);
+    const double lu = log(u53_open0(r2.x, r2.y));
+    if (lu < 0.5 * x * x + dd * (3.0 * log1p(t) - v1)) return 2.0 * dd * (1.0 + v1);
+  }
+  return df;  // unreachable in practice (acceptance > 0.95 per attempt)
+}
+
+template <int D, int K, bool REPLAY>
+__global__ __launch_bounds__(256) void hyper_kernel(HyperArgs a) {
+  constexpr int NXY = K * D;
+  constexpr int NYY = D * (D + 1) / 2;
+  constexpr int NS = NXY + NYY + 1;
+  constexpr int NTRIL = D * (D - 1) / 2;
+  __shared__ double red[4][NS];
+  __shared__ double tot[NS];
+  __shared__ double var_iw[4], var_chi[4], var_noise[32];
+
+  const Geometry& g = a.g;
+  const int c = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int64_t done = __hip_atomic_load(&a.ctrl->cur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int64_t s = a.mode == 1 ? 0 : done + 1;  // sweep whose statistics are reduced here
+  const int64_t hs = (D == 2) ? s + 1 : s;        // sweep the drawn (beta, Sigma) belongs to
+
+  // 1. fixed-order reduction over all units of all shards (independent of world size)
+  double acc[NS];
+#pragma unroll
+  for (int j = 0; j < NS; ++j) acc[j] = 0.0;
+  for (int64_t u = tid; u < g.n_units_global; u += 256) {
+    const int64_t r = u / g.units_per_rank;
+    const int64_t lu = u - r * g.units_per_rank;
+    const double* p = a.units + ((r * g.n_chains + c) * g.units_per_rank + lu) * g.stride;
+#pragma unroll
+    for (int j = 0; j < NS; ++j) acc[j] += p[j];
+  }
+  block_reduce<NS>(acc, red, tot);
+
+  // 2. variates
+  if constexpr (REPLAY) {
+    const double* tv = a.r.tape + ((int64_t)c * a.r.tape_sweeps + (hs - 1)) * a.r.tape_sweep_stride +
+                       (a.r.tape_sweep_stride - TAPE_HYPER);
+    if (tid < 3) var_iw[tid] = tv[tid];
+    if (tid < 3) var_chi[tid] = tv[3 + tid];
+    if (tid < D * K) var_noise[tid] = tv[6 + tid];
+  } else {
+    uint32_t k0, k1;
+    chain_key(a.r.seed, (int64_t)a.r.chain_first + c, &k0, &k1);
+    if (tid < NTRIL) var_iw[tid] = hyper_normal(k0, k1, HSLOT_NORMAL0 + tid, (uint32_t)hs);
+    if (tid >= 64 && tid < 64 + D * K)
+      var_noise[tid - 64] = hyper_normal(k0, k1, HSLOT_BETA_NORMAL0 + (tid - 64), (uint32_t)hs);
+    if (tid >= 128 && tid < 128 + D) {
+      const int q = tid - 128;
+      var_chi[q] = chi2_draw(k0, k1, (uint32_t)hs, q, a.nu_n - D + 1 + q);
+    }
+  }
+  __syncthreads();
+
+  // 3. algebra + outputs (one lane)
+  if (tid == 0) {
+    double beta[K][D], Sig[D][D];
+    level2_draw<D, K>(tot, a.V, a.cholV, a.A0B0, a.S0B, var_iw, var_chi, var_noise, REPLAY, beta, Sig);
+    finalize_hyper<D, K>(beta, Sig, a.omega2, a.hyper + (int64_t)c * HS);
+    if (hs >= 1 && is_stored(hs, g)) {
+      double* o = a.level2 + ((int64_t)c * g.n_draws + draw_index(hs, g)) * g.l2w;
+      int q = 0;
+#pragma unroll
+      for (int d = 0; d < D; ++d)
+#pragma unroll
+        for (int k = 0; k < K; ++k) o[q++] = beta[k][d];  // beta.T.ravel() (bi:411)
+#pragma unroll
+      for (int p = 0; p < D; ++p)
+#pragma unroll
+        for (int r = p; r < D; ++r) o[q++] = Sig[p][r];  // bi:412, tri:550-554
+    }
+    if (a.mode == 0 && is_stored(s, g))
+      a.loglik[(int64_t)c * g.n_draws + draw_index(s, g)] = tot[NS - 1] / (double)g.n_global;  // np.mean
+    if (a.mode == 0) {
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      const uint32_t old = __hip_atomic_fetch_add(&a.ctrl->arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      if (old == (uint32_t)g.n_chains - 1) {
+        __hip_atomic_store(&a.ctrl->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&a.ctrl->cur, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+}
+
+// (beta, Sigma) -> hyper state for every chain: [chain][K*D + D*D] input.
+template <int D, int K>
+__global__ void set_hyper_kernel(int n_chains, double* hyper, const double* bs, double omega2) {
+  const int c = threadIdx.x;
+  if (c >= n_chains) return;
+  const double* in = bs + (int64_t)c * (K * D + D * D);
+  double beta[K][D], Sig[D][D];
+  for (int k = 0; k < K; ++k)
+    for (int d = 0; d < D; ++d) beta[k][d] = in[k * D + d];
+  for (int p = 0; p < D; ++p)
+    for (int q = 0; q < D; ++q) Sig[p][q] = in[K * D + p * D + q];
+  finalize_hyper<D, K>(beta, Sig, omega2, hyper + (int64_t)c * HS);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Debug / test kernels
+// ---------------------------------------------------------------------------------------------
+__global__ void debug_philox_kernel(uint32_t k0, uint32_t k1, const uint32_t* ctr, int64_t n, uint32_t* out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const u32x4 r = philox4x32_10(u32x4{ctr[4 * i], ctr[4 * i + 1], ctr[4 * i + 2], ctr[4 * i + 3]}, k0, k1);
+  out[4 * i] = r.x;
+  out[4 * i + 1] = r.y;
+  out[4 * i + 2] = r.z;
+  out[4 * i + 3] = r.w;
+}
+
+__global__ void debug_variates_kernel(uint64_t seed, int chain, uint32_t sweep, int64_t n, int S, float* tl,
+                                      float* tm, float* ua, double* uz, double* ut, double* ea, double* ez) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t k0, k1;
+  chain_key(seed, chain, &k0, &k1);
+  const u32x4 r = customer_block(k0, k1, (uint32_t)i, sweep, SLOT_ZTAU);
+  uz[i] = u53(r.x, r.y);
+  ut[i] = u53(r.z, r.w);
+  ea[i] = -log(u53_open0(r.z, r.w));
+  const u32x4 re = customer_block(k0, k1, (uint32_t)i, sweep, SLOT_ETA);
+  ez[i] = sqrt(-2.0 * log(u53_open0(re.x, re.y))) * cospi(2.0 * u53(re.z, re.w));
+  for (int j = 0; j < S; ++j) {
+    const u32x4 ra = customer_block(k0, k1, (uint32_t)i, sweep, SLOT_MH0 + 2u * j);
+    const u32x4 rb = customer_block(k0, k1, (uint32_t)i, sweep, SLOT_MH0 + 2u * j + 1u);
+    float a, b, lu;
+    mh_variates(ra, rb, &a, &b, &lu);
+    tl[(int64_t)j * n + i] = a;
+    tm[(int64_t)j * n + i] = b;
+    ua[(int64_t)j * n + i] = uf32(rb.z);
+  }
+}
+
+// in: [V 81][cholV 81][A0B0 27][S0B 9] prior block, then xty(K*D) yty(D*D) iwn(3) chi2(3) z(D*K)
+template <int D, int K>
+__global__ void debug_level2_kernel(const double* prior, const double* in, double* out) {
+  if (threadIdx.x != 0) return;
+  const double* V = prior;
+  const double* cholV = prior + 81;
+  const double* A0B0 = prior + 162;
+  const double* S0B = prior + 189;
+  constexpr int NXY = K * D;
+  double tot[NXY + D * (D + 1) / 2 + 1];
+  for (int q = 0; q < NXY; ++q) tot[q] = in[q];
+  int t = NXY;
+  for (int p = 0; p < D; ++p)
+    for (int q = p; q < D; ++q) tot[t++] = in[NXY + p * D + q];
+  const double* iwn = in + NXY + D * D;
+  const double* chi = iwn + 3;
+  const double* z = chi + 3;
+  double beta[K][D], Sig[D][D];
+  level2_draw<D, K>(tot, V, cholV, A0B0, S0B, iwn, chi, z, false, beta, Sig);
+  for (int k = 0; k < K; ++k)
+    for (int d = 0; d < D; ++d) out[k * D + d] = beta[k][d];
+  for (int p = 0; p < D; ++p)
+    for (int q = 0; q < D; ++q) out[K * D + p * D + q] = Sig[p][q];
+}
+
+__global__ void debug_hyper_variates_kernel(uint64_t seed, int chain, uint32_t sweep, double df, int64_t n,
+                                            double* chi2, double* normals) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t k0, k1;
+  chain_key(seed, chain, &k0, &k1);
+  chi2[i] = chi2_draw(k0, k1, sweep + (uint32_t)i, 0, df);
+  normals[i] = hyper_normal(k0, k1, HSLOT_NORMAL0, sweep + (uint32_t)i);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Dispatch
+// ---------------------------------------------------------------------------------------------
+#define CLV_FOR_K(M, D, R) \
+  M(D, 1, R) M(D, 2, R) M(D, 3, R) M(D, 4, R) M(D, 5, R) M(D, 6, R) M(D, 7, R) M(D, 8, R) M(D, 9, R)
+
+hipError_t launch_sweep(const SweepArgs& a, bool replay, hipStream_t st) {
+  const dim3 grid(a.g.nb_local, a.g.n_chains);
+  const dim3 block(BLOCK);
+#define CLV_CASE(DD, KK, RR) \
+  if (a.g.D == DD && a.g.K == KK && replay == RR) { hipLaunchKernelGGL((sweep_kernel<DD, KK, RR>), grid, block, 0, st, a); return hipGetLastError(); }
+  CLV_FOR_K(CLV_CASE, 2, false)
+  CLV_FOR_K(CLV_CASE, 3, false)
+  CLV_FOR_K(CLV_CASE, 2, true)
+  CLV_FOR_K(CLV_CASE, 3, true)
+#undef CLV_CASE
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_group(const GroupArgs& a, hipStream_t st) {
+  const int units_local = (a.g.nb_local + a.g.blocks_per_unit - 1) / a.g.blocks_per_unit;
+  hipLaunchKernelGGL(group_kernel, dim3(units_local, a.g.n_chains), dim3(64), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_hyper(const HyperArgs& a, bool replay, hipStream_t st) {
+#define CLV_CASE(DD, KK, RR) \
+  if (a.g.D == DD && a.g.K == KK && replay == RR) { hipLaunchKernelGGL((hyper_kernel<DD, KK, RR>), dim3(a.g.n_chains), dim3(256), 0, st, a); return hipGetLastError(); }
+  CLV_FOR_K(CLV_CASE, 2, false)
+  CLV_FOR_K(CLV_CASE, 3, false)
+  CLV_FOR_K(CLV_CASE, 2, true)
+  CLV_FOR_K(CLV_CASE, 3, true)
+#undef CLV_CASE
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_set_hyper(int D, int K, int n_chains, double* hyper, const double* bs, double omega2,
+                            hipStream_t st) {
+#define CLV_CASE(DD, KK, RR) \
+  if (D == DD && K == KK) { hipLaunchKernelGGL((set_hyper_kernel<DD, KK>), dim3(1), dim3(64), 0, st, n_chains, hyper, bs, omega2); return hipGetLastError(); }
+  CLV_FOR_K(CLV_CASE, 2, 0)
+  CLV_FOR_K(CLV_CASE, 3, 0)
+#undef CLV_CASE
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_debug_philox(uint32_t k0, uint32_t k1, const uint32_t* ctr, int64_t n, uint32_t* out,
+                               hipStream_t st) {
+  hipLaunchKernelGGL(debug_philox_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, k0, k1, ctr, n, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_debug_variates(uint64_t seed, int chain, uint32_t sweep, int64_t n, int S, float* tl,
+                                 float* tm, float* ua, double* uz, double* ut, double* ea, double* ez,
+                                 hipStream_t st) {
+  hipLaunchKernelGGL(debug_variates_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, seed, chain,
+                     sweep, n, S, tl, tm, ua, uz, ut, ea, ez);
+  return hipGetLastError();
+}
+
+hipError_t launch_debug_level2(int D, int K, const double* prior_dev, const double* in, double* out,
+                               hipStream_t st) {
+#define CLV_CASE(DD, KK, RR) \
+  if (D == DD && K == KK) { hipLaunchKernelGGL((debug_level2_kernel<DD, KK>), dim3(1), dim3(64), 0, st, prior_dev, in, out); return hipGetLastError(); }
+  CLV_FOR_K(CLV_CASE, 2, 0)
+  CLV_FOR_K(CLV_CASE, 3, 0)
+#undef CLV_CASE
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_debug_hyper_variates(uint64_t seed, int chain, uint32_t sweep, double df, int64_t n,
+                                       double* chi2, double* normals, hipStream_t st) {
+  hipLaunchKernelGGL(debug_hyper_variates_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, seed,
+                     chain, sweep, df, n, chi2, normals);
+  return hipGetLastError();
+}
+
+}  // namespace clv

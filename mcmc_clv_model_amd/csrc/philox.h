@@ -1,0 +1,96 @@
+// Philox4x32-10 counter-based RNG and the variate transforms of the sampler's Philox mode.
+//
+// The reference draws from numpy's PCG64 stream in a fixed call order
+// (bivariate/mcmc.py:200, 217, 225, 258, 261, 316-317, 330; trivariate/mcmc.py:333), which
+// cannot be reproduced by a parallel sampler.  Here every variate is a pure function of
+//   key     = (lo32(seed + chain), hi32(seed + chain))      (reference: default_rng(seed + ch))
+//   counter = (customer, sweep, slot, stream)                 (stream 0 = customers, 1 = hyper)
+// so draws do not depend on launch geometry, sharding or GPU count.  The same transforms are
+// restated in numpy by oracle/philox.py (test infrastructure) and pinned by tests.
+#pragma once
+#include <stdint.h>
+
+
+#define CLV_HD __host__ __device__ __forceinline__
+
+namespace clv {
+
+struct u32x4 { uint32_t x, y, z, w; };
+
+CLV_HD u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
+    const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    c = u32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+
+// Stream ids (counter word 3).
+enum : uint32_t { STREAM_CUSTOMER = 0u, STREAM_HYPER = 1u };
+
+// Customer-stream slots (counter word 2).
+enum : uint32_t { SLOT_ZTAU = 0u, SLOT_ETA = 1u, SLOT_MH0 = 2u };  // MH step j: SLOT_MH0+2j, +2j+1
+
+// Hyper-stream slots (counter word 0; word 1 = sweep).
+enum : uint32_t { HSLOT_NORMAL0 = 0u, HSLOT_BETA_NORMAL0 = 4u, HSLOT_GAMMA0 = 64u, HSLOT_GAMMA_STRIDE = 256u };
+constexpr int GAMMA_MAX_ATTEMPTS = 100;
+
+// 53-bit uniform in [0, 1) from two words (numpy's random() resolution).
+CLV_HD double u53(uint32_t lo, uint32_t hi) {
+  const uint64_t v = (((uint64_t)hi << 32) | lo) >> 11;
+  return (double)v * 0x1.0p-53;
+}
+// 53-bit uniform in (0, 1].
+CLV_HD double u53_open0(uint32_t lo, uint32_t hi) {
+  const uint64_t v = (((uint64_t)hi << 32) | lo) >> 11;
+  return (double)(v + 1) * 0x1.0p-53;
+}
+
+CLV_HD u32x4 customer_block(uint32_t k0, uint32_t k1, uint32_t customer, uint32_t sweep, uint32_t slot) {
+  return philox4x32_10(u32x4{customer, sweep, slot, STREAM_CUSTOMER}, k0, k1);
+}
+CLV_HD u32x4 hyper_block(uint32_t k0, uint32_t k1, uint32_t slot, uint32_t sweep) {
+  return philox4x32_10(u32x4{slot, sweep, 0u, STREAM_HYPER}, k0, k1);
+}
+
+CLV_HD void chain_key(uint64_t seed, int64_t chain, uint32_t* k0, uint32_t* k1) {
+  const uint64_t s = seed + (uint64_t)chain;
+  *k0 = (uint32_t)s;
+  *k1 = (uint32_t)(s >> 32);
+}
+
+// fp32 uniform in [2^-33, 1] for the proposal-noise transforms (hardware transcendentals).
+__device__ __forceinline__ float uf32(uint32_t w) {
+  return __builtin_fmaf((float)w, 0x1.0p-32f, 0x1.0p-33f);
+}
+__device__ __forceinline__ float ln_f32(float u) {  // natural log via v_log_f32 (log2)
+  return __builtin_amdgcn_logf(u) * 0.69314718055994530942f;
+}
+// Two independent standard normals (Box-Muller; v_sin/v_cos take revolutions).
+__device__ __forceinline__ void box_muller_f32(uint32_t a, uint32_t b, float* z0, float* z1) {
+  const float r = __builtin_amdgcn_sqrtf(-2.0f * ln_f32(uf32(a)));
+  const float t = uf32(b);
+  *z0 = r * __builtin_amdgcn_cosf(t);
+  *z1 = r * __builtin_amdgcn_sinf(t);
+}
+// One MH step's variates from 8 words: two Student-t(3) draws and log of the accept uniform.
+// t3 = Z / sqrt(chi2_3 / 3),  chi2_3 = Exp(mean 2) + Z'^2 = -2 ln U + Z'^2.
+__device__ __forceinline__ void mh_variates(const u32x4& ra, const u32x4& rb, float* t_l, float* t_m,
+                                            float* log_u) {
+  float za, zb, zc, zd;
+  box_muller_f32(ra.x, ra.y, &za, &zb);
+  box_muller_f32(rb.x, rb.y, &zc, &zd);
+  const float chi_l = __builtin_fmaf(zc, zc, -2.0f * ln_f32(uf32(ra.z)));
+  const float chi_m = __builtin_fmaf(zd, zd, -2.0f * ln_f32(uf32(ra.w)));
+  *t_l = za * __builtin_amdgcn_rsqf(chi_l * (1.0f / 3.0f));
+  *t_m = zb * __builtin_amdgcn_rsqf(chi_m * (1.0f / 3.0f));
+  *log_u = ln_f32(uf32(rb.z));
+}
+
+}  // namespace clv

@@ -1,0 +1,128 @@
+"""Customer sharding across GPUs: one process per GPU, one exchange per sweep.
+
+Customers are conditionally independent given (beta, Sigma) (bivariate/mcmc.py:193-339), so
+each rank sweeps its own contiguous customer range; the only coupling is the level-2 draw
+(bivariate/mcmc.py:233-262), which needs the sufficient statistics X'Y, Y'Y of ALL customers.
+Per sweep each rank publishes its unit partials, one ``all_gather_into_tensor`` over
+torch.distributed (backend "nccl" = RCCL over xGMI on MI355X; "gloo" in the CPU tests)
+assembles [world][chain][units_per_rank][stride], and every rank performs the identical
+fixed-order sum and the identical level-2 draw (same Philox counter), so no broadcast is needed
+and results are bitwise independent of the GPU count.
+
+Shard plan (a function of n_global and world only):
+  blocks_per_unit G  = clv_default_blocks_per_unit(n_global)     (units <= 512)
+  blocks_per_rank    = ceil(ceil(n_blocks / world) / G) * G
+  shard r            = customers [r * blocks_per_rank * 256, min(n, (r+1) * blocks_per_rank * 256))
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+from . import _lib
+
+BLOCK = _lib.BLOCK
+
+
+def default_blocks_per_unit(n_global: int) -> int:
+    """Same rule as clv_default_blocks_per_unit (C) — kept in Python for CPU-side planning."""
+    nb = -(-n_global // BLOCK)
+    g = 1
+    while -(-nb // g) > 512:
+        g *= 2
+    return g
+
+
+@dataclass(frozen=True)
+class ShardPlan:
+    n_global: int
+    world: int
+    blocks_per_unit: int
+    blocks_per_rank: int
+
+    @property
+    def units_per_rank(self) -> int:
+        return self.blocks_per_rank // self.blocks_per_unit
+
+    @property
+    def n_units_global(self) -> int:
+        nb = -(-self.n_global // BLOCK)
+        return -(-nb // self.blocks_per_unit)
+
+    def shard(self, rank: int):
+        """[begin, end) customer range of ``rank``."""
+        b = rank * self.blocks_per_rank * BLOCK
+        e = min(self.n_global, (rank + 1) * self.blocks_per_rank * BLOCK)
+        return min(b, self.n_global), max(min(b, self.n_global), e)
+
+
+def plan(n_global: int, world: int, blocks_per_unit: Optional[int] = None) -> ShardPlan:
+    if n_global < 1 or world < 1:
+        raise ValueError("n_global and world must be >= 1")
+    G = blocks_per_unit or default_blocks_per_unit(n_global)
+    nb = -(-n_global // BLOCK)
+    per = -(-nb // world)
+    bpr = -(-per // G) * G
+    return ShardPlan(n_global=n_global, world=world, blocks_per_unit=G, blocks_per_rank=bpr)
+
+
+def slice_problem(p, begin: int, end: int):
+    """The rank-local view of a Problem (setup constants stay global, like the reference's)."""
+    from dataclasses import replace
+    return replace(p, x=np.ascontiguousarray(p.x[begin:end]), t_x=np.ascontiguousarray(p.t_x[begin:end]),
+                   T_cal=np.ascontiguousarray(p.T_cal[begin:end]),
+                   cov=np.ascontiguousarray(p.cov[:, begin:end]),
+                   log_s=None if p.log_s is None else np.ascontiguousarray(p.log_s[begin:end]))
+
+
+def exchange(local, gathered, group=None) -> None:
+    """All-gather this rank's unit partials (1-D tensor) into ``gathered`` (world * len)."""
+    import torch.distributed as dist
+    dist.all_gather_into_tensor(gathered, local, group=group)
+
+
+class ShardedSampler:
+    """This rank's shard of a problem on its GPU; sweeps with one all-gather per sweep."""
+
+    def __init__(self, p_global, *, rank: int, world: int, chains: int, mcmc: int, burnin: int, thin: int,
+                 seed: int, n_mh_steps: int = 20, draw_sink: str = "summary", device: int = 0, group=None):
+        import torch
+        from .sampler import HipSampler, make_prior
+        self.torch = torch
+        self.plan = plan(p_global.N, world)
+        b, e = self.plan.shard(rank)
+        self.begin, self.end = b, e
+        self.rank, self.world, self.group = rank, world, group
+        torch.cuda.set_device(device)
+        stream = torch.cuda.current_stream().cuda_stream
+        prior = make_prior(p_global, p_global.N)
+        self.s = HipSampler(slice_problem(p_global, b, e), mcmc=mcmc, burnin=burnin, thin=thin, chains=chains,
+                            seed=seed, n_mh_steps=n_mh_steps, draw_sink=draw_sink, device=device,
+                            n_global=p_global.N, shard_begin=rank * self.plan.blocks_per_rank * BLOCK,
+                            world_size=world, rank=rank, blocks_per_rank=self.plan.blocks_per_rank,
+                            blocks_per_unit=self.plan.blocks_per_unit, stream=stream, prior=prior)
+        _, nd, _ = self.s.partials()
+        self.local = torch.zeros(nd, dtype=torch.float64, device=f"cuda:{device}")
+        self.gathered = torch.zeros(nd * world, dtype=torch.float64, device=f"cuda:{device}")
+        self.D = p_global.D
+        if self.D == 2:  # bivariate: the draw for sweep 1 comes from the initial state (bi:393)
+            self._exchange_and_hyper()
+
+    def _exchange_and_hyper(self) -> None:
+        self.s.copy_partials(self.local.data_ptr())
+        exchange(self.local, self.gathered, self.group)
+        self.s.hyper(self.gathered.data_ptr())
+
+    def step(self, n: int = 1) -> None:
+        for _ in range(n):
+            self.s.sweep()
+            self._exchange_and_hyper()
+
+    def synchronize(self) -> None:
+        self.s.synchronize()
+        self.torch.cuda.synchronize()
+
+    def close(self) -> None:
+        self.s.close()

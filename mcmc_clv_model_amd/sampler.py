@@ -1,0 +1,314 @@
+"""Host side of the HIP sampler: reference-identical setup + the libclvmcmc handle.
+
+The reference computes its setup on the host (design matrix, priors, initial values); this
+module does the same with the same numpy/pandas operations so the constants handed to the
+device are bit-identical to the reference's:
+
+* design matrix / priors ........ bivariate/mcmc.py:467-479, trivariate/mcmc.py:615-626
+* initial lambda, mu, beta_0 .... bivariate/mcmc.py:367-374, trivariate/mcmc.py:488-499
+* V = inv(X'X + A0) ............. bivariate/mcmc.py:248-249 (constant across sweeps)
+
+Everything per sweep runs on the GPU (kernels.hip).
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, dptr
+
+
+@dataclass
+class Problem:
+    """One CBS table prepared for the sampler (all arrays host-side, float64 unless noted)."""
+    D: int
+    K: int
+    x: np.ndarray            # int32 repeat transactions
+    t_x: np.ndarray
+    T_cal: np.ndarray
+    cov: np.ndarray          # (K-1, N) C-contiguous, non-intercept columns of X
+    log_s: Optional[np.ndarray]
+    lam_init: float
+    beta_0: np.ndarray       # K x D (intercept row set from the data)
+    A_0: np.ndarray
+    nu_00: float
+    gamma_00: np.ndarray
+    V: np.ndarray            # inv(X'X + A0)
+    omega2: float = 1.0
+    covariates: List[str] = field(default_factory=list)
+
+    @property
+    def N(self) -> int:
+        return int(self.x.shape[0])
+
+
+def build_problem(cal_cbs, covariates: Optional[Sequence[str]], D: int) -> Problem:
+    """Mirror of the reference's setup (see module docstring) for a pandas CBS DataFrame."""
+    covariates = list(covariates or [])
+    cbs = cal_cbs.copy().reset_index(drop=True)
+    cbs["intercept"] = 1.0
+    cols = ["intercept"] + covariates
+    X = cbs[cols].to_numpy(float)
+    N, K = X.shape
+    if K > _lib.MAX_K:
+        raise ValueError(f"at most {_lib.MAX_K - 1} covariates are supported (got {K - 1})")
+    x = cbs["x"].to_numpy()
+    t_x = np.ascontiguousarray(cbs["t_x"].to_numpy(), dtype=np.float64)
+    T_cal = np.ascontiguousarray(cbs["T_cal"].to_numpy(), dtype=np.float64)
+    if N and (np.any(x < 0) or np.any(x > np.iinfo(np.int32).max) or np.any(x != np.round(x))):
+        raise ValueError("x must hold non-negative integer counts")
+
+    # bi:368-374 / tri:489-499
+    lam_init = cbs["x"].mean() / np.mean(np.where(cbs["t_x"] == 0, cbs["T_cal"], cbs["t_x"]))
+    lambdas = np.full(N, lam_init)
+    mus = 1.0 / (t_x + 0.5 / lam_init)
+    beta_0 = np.zeros((K, D))
+    beta_0[0, 0] = math.log(lambdas.mean())
+    beta_0[0, 1] = math.log(mus.mean())
+    log_s = None
+    omega2 = 1.0
+    if D == 3:
+        log_s = np.ascontiguousarray(cbs["log_s"].to_numpy(), dtype=np.float64)
+        omega2 = float(cbs["log_s"].var())
+        beta_0[0, 2] = cbs["log_s"].mean()
+    A_0 = np.eye(K) * 0.01
+    nu_00 = (3 if D == 2 else 4) + K
+    gamma_00 = nu_00 * np.eye(D)
+    V = np.linalg.inv(X.T @ X + A_0)
+    return Problem(D=D, K=K, x=np.ascontiguousarray(x, dtype=np.int32), t_x=t_x, T_cal=T_cal,
+                   cov=np.ascontiguousarray(X[:, 1:].T), log_s=log_s, lam_init=float(lam_init),
+                   beta_0=beta_0, A_0=A_0, nu_00=float(nu_00), gamma_00=gamma_00, V=V,
+                   omega2=omega2, covariates=covariates)
+
+
+def make_prior(p: Problem, n_global: Optional[int] = None) -> _lib.ClvPrior:
+    pr = _lib.ClvPrior()
+    K, D = p.K, p.D
+    pr.lam_init = p.lam_init
+    cholV = np.linalg.cholesky(p.V)
+    A0B0 = p.A_0 @ p.beta_0
+    S0B = p.gamma_00 + p.beta_0.T @ p.A_0 @ p.beta_0
+    for i, v in enumerate(p.V.ravel()):
+        pr.V[i] = v
+    for i, v in enumerate(cholV.ravel()):
+        pr.chol_V[i] = v
+    for i, v in enumerate(A0B0.ravel()):
+        pr.A0B0[i] = v
+    for i, v in enumerate(S0B.ravel()):
+        pr.S0_B0A0B0[i] = v
+    pr.nu_n = p.nu_00 + (p.N if n_global is None else n_global)
+    for i, v in enumerate(p.beta_0.ravel()):
+        pr.beta_init[i] = v
+    for i, v in enumerate(p.gamma_00.ravel()):
+        pr.sigma_init[i] = v
+    pr.omega2 = p.omega2
+    return pr
+
+
+def resolve_seed(seed: Optional[int]) -> int:
+    if seed is None:  # reference: default_rng(None) -> OS entropy (bi:486)
+        return int(np.random.SeedSequence().entropy) & ((1 << 63) - 1)
+    return int(seed) & ((1 << 64) - 1)
+
+
+_SINKS = {"full": _lib.SINK_FULL, "summary": _lib.SINK_SUMMARY, "none": _lib.SINK_NONE}
+_RNGS = {"philox": _lib.RNG_PHILOX, "replay": _lib.RNG_REPLAY}
+
+
+class HipSampler:
+    """One libclvmcmc handle: ``chains`` chains of one problem (or one shard of it) on one GPU."""
+
+    def __init__(self, p: Problem, *, mcmc: int, burnin: int, thin: int, chains: int, seed: int,
+                 n_mh_steps: int = 20, draw_sink: str = "full", rng: str = "philox", device: int = -1,
+                 chain_first: int = 0, n_global: Optional[int] = None, shard_begin: int = 0,
+                 world_size: int = 1, rank: int = 0, blocks_per_rank: int = 0, blocks_per_unit: int = 0,
+                 stream: int = 0, prior: Optional[_lib.ClvPrior] = None):
+        L = _lib.lib()
+        if draw_sink not in _SINKS:
+            raise ValueError(f"draw_sink must be one of {sorted(_SINKS)}")
+        if rng not in _RNGS:
+            raise ValueError(f"rng must be one of {sorted(_RNGS)}")
+        if _lib.device_count() < 1:
+            raise _lib.ClvError("no HIP device visible; the sampler has no CPU fallback")
+        self.p = p
+        self.D, self.K, self.n = p.D, p.K, p.N
+        self.chains = int(chains)
+        self.mcmc, self.burnin, self.thin = int(mcmc), int(burnin), int(thin)
+        self.n_draws = (self.mcmc - 1) // self.thin + 1 if self.mcmc >= 1 else 0
+        self.draw_sink = draw_sink
+        cfg = _lib.ClvConfig()
+        cfg.abi_version = _lib.ABI_VERSION
+        cfg.D, cfg.K, cfg.n_mh_steps = p.D, p.K, int(n_mh_steps)
+        cfg.burnin, cfg.mcmc, cfg.thin = self.burnin, self.mcmc, self.thin
+        cfg.n_chains, cfg.chain_first = self.chains, int(chain_first)
+        cfg.rng_mode, cfg.draw_sink, cfg.device = _RNGS[rng], _SINKS[draw_sink], int(device)
+        cfg.seed = int(seed)
+        cfg.n_global = int(p.N if n_global is None else n_global)
+        cfg.shard_begin = int(shard_begin)
+        cfg.world_size, cfg.rank = int(world_size), int(rank)
+        cfg.blocks_per_rank, cfg.blocks_per_unit = int(blocks_per_rank), int(blocks_per_unit)
+        cfg.stream = int(stream)
+        self.cfg = cfg
+        data = _lib.ClvData()
+        data.n = p.N
+        self._keep = [p.x, p.t_x, p.T_cal, p.cov, p.log_s]
+        data.x = p.x.ctypes.data if p.N else None
+        data.t_x = p.t_x.ctypes.data if p.N else None
+        data.T_cal = p.T_cal.ctypes.data if p.N else None
+        data.covariates = p.cov.ctypes.data if (p.K > 1 and p.N) else None
+        data.log_s = p.log_s.ctypes.data if (p.D == 3 and p.N) else None
+        self.prior = prior if prior is not None else make_prior(p, cfg.n_global)
+        h = ctypes.c_void_p()
+        check(L.clv_create(ctypes.byref(cfg), ctypes.byref(data), ctypes.byref(self.prior), ctypes.byref(h)))
+        self.h = h
+        self._L = L
+
+    # ---- lifecycle
+    def close(self) -> None:
+        if getattr(self, "h", None):
+            self._L.clv_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # ---- running
+    def run(self, n_sweeps: int) -> None:
+        check(self._L.clv_run(self.h, int(n_sweeps)))
+
+    def sweep(self) -> None:
+        check(self._L.clv_sweep(self.h))
+
+    def hyper(self, gathered_ptr: Optional[int] = None) -> None:
+        check(self._L.clv_hyper(self.h, gathered_ptr))
+
+    def partials(self):
+        ptr = ctypes.c_void_p()
+        nd = ctypes.c_int64()
+        st = ctypes.c_int32()
+        check(self._L.clv_partials(self.h, ctypes.byref(ptr), ctypes.byref(nd), ctypes.byref(st)))
+        return ptr.value, nd.value, st.value
+
+    def copy_partials(self, dst_ptr: int) -> None:
+        check(self._L.clv_copy_partials(self.h, ctypes.c_void_p(dst_ptr)))
+
+    def synchronize(self) -> None:
+        check(self._L.clv_synchronize(self.h))
+
+    @property
+    def sweeps_done(self) -> int:
+        return int(self._L.clv_sweeps_done(self.h))
+
+    def set_replay_tape(self, tape: np.ndarray, n_sweeps: int) -> None:
+        tape = np.ascontiguousarray(tape, dtype=np.float64)
+        stride = self.replay_sweep_stride
+        if tape.size != self.chains * n_sweeps * stride:
+            raise ValueError(f"tape has {tape.size} doubles, expected {self.chains * n_sweeps * stride}")
+        check(self._L.clv_set_replay_tape(self.h, dptr(tape), int(n_sweeps)))
+
+    @property
+    def replay_sweep_stride(self) -> int:
+        return int(self._L.clv_replay_sweep_stride(self.h))
+
+    # ---- outputs
+    def read_draws(self, level1: bool = True):
+        C, nd, n, D, K = self.chains, self.n_draws, self.n, self.D, self.K
+        l1 = np.empty((C, nd, n, D + 2)) if (level1 and self.draw_sink == "full") else None
+        l2 = np.empty((C, nd, D * K + D * (D + 1) // 2))
+        ll = np.empty((C, nd))
+        check(self._L.clv_read_draws(self.h, dptr(l1), dptr(l2), dptr(ll)))
+        return l1, l2, ll
+
+    def read_summary(self):
+        sums = np.empty((self.chains, _lib.N_SUM_STATS, self.n))
+        k = ctypes.c_int64()
+        check(self._L.clv_read_summary(self.h, dptr(sums), ctypes.byref(k)))
+        return sums, int(k.value)
+
+    def get_state(self):
+        C, n, D, K = self.chains, self.n, self.D, self.K
+        lam, mu = np.empty((C, n)), np.empty((C, n))
+        hyp = np.empty((C, K * D + D * D))
+        check(self._L.clv_get_state(self.h, dptr(lam), dptr(mu), dptr(hyp)))
+        beta = hyp[:, : K * D].reshape(C, K, D)
+        sigma = hyp[:, K * D:].reshape(C, D, D)
+        return lam, mu, beta, sigma
+
+    def set_state(self, lam, mu, beta, sigma, sweeps_done: int) -> None:
+        C, n, D, K = self.chains, self.n, self.D, self.K
+        lam = np.ascontiguousarray(np.broadcast_to(lam, (C, n)), dtype=np.float64)
+        mu = np.ascontiguousarray(np.broadcast_to(mu, (C, n)), dtype=np.float64)
+        hyp = np.concatenate([np.broadcast_to(beta, (C, K, D)).reshape(C, K * D),
+                              np.broadcast_to(sigma, (C, D, D)).reshape(C, D * D)], axis=1)
+        hyp = np.ascontiguousarray(hyp, dtype=np.float64)
+        check(self._L.clv_set_state(self.h, dptr(lam), dptr(mu), dptr(hyp), int(sweeps_done)))
+
+    def set_timing(self, enable: bool) -> None:
+        check(self._L.clv_set_timing(self.h, 1 if enable else 0))
+
+    def kernel_time(self):
+        a, b = ctypes.c_double(), ctypes.c_double()
+        na, nb = ctypes.c_int64(), ctypes.c_int64()
+        check(self._L.clv_kernel_time(self.h, ctypes.byref(a), ctypes.byref(na), ctypes.byref(b), ctypes.byref(nb)))
+        return dict(sweep_ms=a.value, sweep_launches=na.value, hyper_ms=b.value, hyper_launches=nb.value)
+
+
+def run_with_trace(s: HipSampler, total: int, trace: int, n_chains_label: int = 1, chain_offset: int = 0) -> None:
+    """Run ``total`` sweeps, printing the reference's trace line (bi:384-385) for every chain at
+    every multiple of ``trace`` (chains advance together here, so lines come grouped by step)."""
+    done = 0
+    while done < total:
+        if trace:
+            nxt = min(total, (done // trace + 1) * trace)
+        else:
+            nxt = total
+        s.run(nxt - done)
+        done = nxt
+        if trace and done % trace == 0:
+            for ch in range(n_chains_label):
+                print(f"chain {chain_offset + ch + 1} | step {done}/{total}")
+
+
+def fit(p: Problem, *, mcmc: int, burnin: int, thin: int, chains: int, seed, trace: int, n_mh_steps: int,
+        draw_sink: str = "full", rng: str = "philox", device: int = -1, replay_tape=None,
+        replay_sweeps: Optional[int] = None) -> dict:
+    """Run all chains of one problem in one batched launch sequence and return the reference's
+    output layout (bi:499-504): level_1 / level_2 lists with one array per chain, and the
+    marginal log-likelihood = mean over all chains' per-draw means."""
+    if chains < 1:
+        raise ValueError("chains must be >= 1")
+    if thin < 1:
+        raise ValueError("thin must be >= 1")
+    s = HipSampler(p, mcmc=mcmc, burnin=burnin, thin=thin, chains=chains, seed=resolve_seed(seed),
+                   n_mh_steps=n_mh_steps, draw_sink=draw_sink, rng=rng, device=device)
+    try:
+        if rng == "replay":
+            if replay_tape is None:
+                raise ValueError("rng='replay' needs replay_tape")
+            s.set_replay_tape(replay_tape, replay_sweeps)
+        run_with_trace(s, burnin + mcmc, trace, n_chains_label=chains)
+        l1, l2, ll = s.read_draws(level1=draw_sink == "full")
+        out = dict(level_1=[l1[c] for c in range(chains)] if l1 is not None else None,
+                   level_2=[l2[c] for c in range(chains)],
+                   log_likelihood=np.mean(ll.reshape(-1)) if ll.size else np.float64("nan"))
+        if draw_sink == "summary":
+            sums, k = s.read_summary()
+            names = _lib.SUM_STATS if p.D == 3 else _lib.SUM_STATS[:7]
+            out["summary"] = dict(n_draws=k, **{nm: sums[:, j, :] / max(k, 1) for j, nm in enumerate(names)})
+        return out
+    finally:
+        s.close()

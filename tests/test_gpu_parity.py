@@ -1,0 +1,257 @@
+"""GPU parity tests of the HIP path (through the C ABI), against the oracle and the reference's
+recorded outputs (golden fixtures).  Tolerances are stated per test."""
+import ctypes
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import philox as oph
+from tests.helpers import GOLDEN, bits, cdnow, golden, replay_case
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def L():
+    from mcmc_clv_model_amd import _lib
+    lib = _lib.lib()
+    assert _lib.device_count() >= 1, "no HIP device: GPU tests must run on an MI355X"
+    return lib
+
+
+def _u32p(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
+
+
+def _fp(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+
+
+def _dp(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+# ---------------------------------------------------------------------------------------------
+def test_device_philox_known_answers(L):
+    """Bit-exact: device Philox4x32-10 vs Random123 KAT + 64 extra oracle vectors."""
+    kat = json.load(open(os.path.join(GOLDEN, "philox_kat.json")))
+    for k in kat["random123"]:
+        ctr = np.array(k["ctr"], np.uint32)
+        out = np.zeros(4, np.uint32)
+        assert L.clv_debug_philox(k["key"][0], k["key"][1], _u32p(ctr), 1, _u32p(out)) == 0
+        assert [f"{v:08x}" for v in out] == k["out"]
+    e = kat["extra"]
+    ctr = np.ascontiguousarray(np.array(e["ctr"], np.uint32))
+    out = np.zeros_like(ctr)
+    assert L.clv_debug_philox(e["key"][0], e["key"][1], _u32p(ctr), len(ctr), _u32p(out)) == 0
+    assert np.array_equal(out, np.array(e["out"], np.uint32))
+
+
+def test_device_variates_match_oracle(L):
+    """u53 uniforms bit-exact; fp64 transforms <= 1e-13 rel; fp32 hardware-transcendental
+    transforms (t3 noise) <= 2e-5 rel/abs (v_log/v_sin/v_cos/v_rsq are ~1-2 ulp fp32)."""
+    n, S, seed, chain, sweep = 4096, 4, 987654321, 2, 77
+    tl, tm, ua = (np.zeros(n * S, np.float32) for _ in range(3))
+    uz, ut, ea, ez = (np.zeros(n) for _ in range(4))
+    assert L.clv_debug_variates(seed, chain, sweep, n, S, _fp(tl), _fp(tm), _fp(ua), _dp(uz), _dp(ut), _dp(ea),
+                                _dp(ez)) == 0
+    ref = oph.sweep_variates(seed, chain, sweep, n, S)
+    assert np.array_equal(uz, ref["u_z"]) and np.array_equal(ut, ref["u_tau"])
+    np.testing.assert_allclose(ea, ref["e_alive"], rtol=1e-13, atol=0)
+    np.testing.assert_allclose(ez, ref["eta_z"], rtol=1e-12, atol=1e-13)
+    np.testing.assert_array_equal(ua.reshape(S, n), ref["u_acc"])
+    np.testing.assert_allclose(tl.reshape(S, n), ref["t_l"], rtol=2e-5, atol=2e-5)
+    np.testing.assert_allclose(tm.reshape(S, n), ref["t_m"], rtol=2e-5, atol=2e-5)
+
+
+def test_device_hyper_variates_match_oracle(L):
+    """Marsaglia–Tsang chi-square and Box–Muller normals of the hyper stream (fp64): <= 1e-12 rel."""
+    n, seed, chain, sweep = 64, 31337, 1, 5
+    for df in (5.0, 23575.0, 1e7 + 3):
+        chi, nor = np.zeros(n), np.zeros(n)
+        assert L.clv_debug_hyper_variates(seed, chain, sweep, df, n, _dp(chi), _dp(nor)) == 0
+        ref = np.array([oph.chi2_draw(seed, chain, sweep + i, 0, df) for i in range(n)])
+        np.testing.assert_allclose(chi, ref, rtol=1e-12)
+        refn = np.array([oph.hyper_normal(seed, chain, 0, sweep + i) for i in range(n)])
+        np.testing.assert_allclose(nor, refn, rtol=1e-12, atol=1e-14)
+
+
+@pytest.mark.parametrize("D", [2, 3])
+@pytest.mark.parametrize("K", [1, 2, 5, 9])
+def test_device_level2_vs_reference(L, D, K):
+    """Device level-2 draw from sufficient statistics vs the reference's _draw_level_2
+    (bi:233-262) with the same Bartlett variates: Sigma <= 1e-11 rel; beta = B_hat +
+    kron(chol Sigma, chol V) z (the device's factor of the same kron covariance) <= 1e-10."""
+    from mcmc_clv_model_amd import _lib
+    f = golden("formulas.npz")
+    p = f"l2_D{D}_K{K}_"
+    X, Y, B0 = f[p + "X"], f[p + "Y"], f[p + "B0"]
+    A0 = np.eye(K) * 0.01
+    S0 = float(f[p + "nu0"]) * np.eye(D)
+    V = f[p + "V"]
+    pr = _lib.ClvPrior()
+    for i, v in enumerate(V.ravel()):
+        pr.V[i] = v
+    for i, v in enumerate(np.linalg.cholesky(V).ravel()):
+        pr.chol_V[i] = v
+    for i, v in enumerate((A0 @ B0).ravel()):
+        pr.A0B0[i] = v
+    for i, v in enumerate((S0 + B0.T @ A0 @ B0).ravel()):
+        pr.S0_B0A0B0[i] = v
+    xty = np.ascontiguousarray(X.T @ Y)
+    yty = np.ascontiguousarray(Y.T @ Y)
+    iwn = np.zeros(3)
+    iwn[: D * (D - 1) // 2] = f[p + "iw_normal"]
+    chi = np.ascontiguousarray(f[p + "iw_chi2"])
+    z = np.ascontiguousarray(f[p + "mvn_z"])
+    beta, sig = np.zeros(K * D), np.zeros(D * D)
+    assert L.clv_debug_level2(D, K, ctypes.byref(pr), _dp(xty), _dp(yty), _dp(iwn), _dp(chi), _dp(z), _dp(beta),
+                              _dp(sig)) == 0
+    np.testing.assert_allclose(sig.reshape(D, D), f[p + "Sigma"], rtol=1e-11)
+    Bh = f[p + "Bhat"]
+    w = np.kron(np.linalg.cholesky(f[p + "Sigma"]), np.linalg.cholesky(V)) @ z
+    np.testing.assert_allclose(beta.reshape(K, D), (Bh.ravel() + w).reshape(K, D), rtol=1e-10, atol=1e-10)
+
+
+# ---------------------------------------------------------------------------------------------
+def _replay_run(name):
+    from mcmc_clv_model_amd import mcmc_draw_parameters, mcmc_draw_parameters_rfm_m
+    df, covs, f = replay_case(name)
+    fn = mcmc_draw_parameters if str(f["kind"]) == "bi" else mcmc_draw_parameters_rfm_m
+    d = fn(df, covs, mcmc=int(f["mcmc"]), burnin=0, thin=1, chains=int(f["chains"]), seed=int(f["seed"]), trace=0,
+           n_mh_steps=int(f["S"]), rng="replay", replay_tape=f["tape"], replay_sweeps=int(f["n_tape_sweeps"]))
+    return d, f
+
+
+@pytest.mark.parametrize("name", ["bi_k1", "bi_k2", "tri_k3", "bi_k1_s0"])
+def test_replay_trajectory_matches_reference(L, name):
+    """G2: the HIP sampler consuming the reference's own variates reproduces the reference's
+    trajectory (every sweep stored): lambda, mu, tau, eta and level-2 draws <= 1e-12 rel
+    (1e-10 for the level-2 record, whose S_n is summed in a different order), z exact, and the
+    marginal log-likelihood <= 1e-12 rel.  At most 0.5% of customers may differ (borderline
+    accept flips from 1-ulp exp/log differences — none expected in 3 sweeps)."""
+    d, f = _replay_run(name)
+    l1 = np.stack(d["level_1"])
+    ref = f["level_1"]
+    assert l1.shape == ref.shape
+    close = np.isclose(l1, ref, rtol=1e-12, atol=0).all(axis=(1, 3))  # (chains, N) over draws & columns
+    assert close.mean() >= 0.995, f"{(~close).sum()} customers diverge"
+    assert (l1[..., 3] == ref[..., 3]).mean() >= 0.995
+    np.testing.assert_allclose(np.stack(d["level_2"]), f["level_2"], rtol=1e-10, atol=1e-12)
+    np.testing.assert_allclose(d["log_likelihood"], float(f["log_likelihood"]), rtol=1e-12)
+
+
+def test_replay_exact_count(L):
+    """Most values are bit-identical (only the transcendentals' last ulp may differ)."""
+    d, f = _replay_run("bi_k2")
+    l1 = np.stack(d["level_1"])
+    frac_bitwise = np.mean(bits(l1[..., :2]) == bits(f["level_1"][..., :2]))
+    assert frac_bitwise > 0.5
+
+
+# ---------------------------------------------------------------------------------------------
+def _bi(df, covs=(), **kw):
+    from mcmc_clv_model_amd import mcmc_draw_parameters
+    base = dict(mcmc=20, burnin=10, thin=2, chains=2, seed=123, trace=0)
+    base.update(kw)
+    return mcmc_draw_parameters(df, list(covs), **base)
+
+
+def test_determinism_bitwise(L):
+    df = cdnow("abe", 1000)
+    a, b = _bi(df, ["first_sales_scaled"]), _bi(df, ["first_sales_scaled"])
+    for x, y in zip(a["level_1"] + a["level_2"], b["level_1"] + b["level_2"]):
+        assert np.array_equal(bits(x), bits(y))
+
+
+def test_chain_batching_invariance(L):
+    """Counter-based RNG: chain c's draws do not depend on how many chains share the launch."""
+    from mcmc_clv_model_amd.sampler import HipSampler, build_problem
+    df = cdnow("abe", 700)
+    p = build_problem(df, ["first_sales_scaled"], 2)
+    kw = dict(mcmc=6, burnin=3, thin=1, seed=99)
+    with HipSampler(p, chains=3, **kw) as s3:
+        s3.run(9)
+        a1, a2, _ = s3.read_draws()
+    with HipSampler(p, chains=1, chain_first=2, **kw) as s1:
+        s1.run(9)
+        b1, b2, _ = s1.read_draws()
+    assert np.array_equal(bits(a1[2]), bits(b1[0])) and np.array_equal(bits(a2[2]), bits(b2[0]))
+
+
+def test_resume_from_state_is_exact(L):
+    from mcmc_clv_model_amd.sampler import HipSampler, build_problem
+    df = cdnow("abe", 500)
+    for D, covs in ((2, ["first_sales_scaled"]), (3, ["gender_F", "age_scaled"])):
+        p = build_problem(df, covs, D)
+        kw = dict(mcmc=10, burnin=0, thin=1, chains=2, seed=5, draw_sink="none")
+        with HipSampler(p, **kw) as s:
+            s.run(10)
+            ref = s.get_state()
+        with HipSampler(p, **kw) as s:
+            s.run(4)
+            st = s.get_state()
+        with HipSampler(p, **kw) as s:
+            s.set_state(*st, sweeps_done=4)
+            s.run(6)
+            got = s.get_state()
+        for x, y in zip(ref, got):
+            assert np.array_equal(bits(x), bits(y))
+
+
+def test_storage_indexing_and_summary_sink(L):
+    """burnin/thin storage (bi:402) and the on-device summary sink == means of the full draws."""
+    df = cdnow("abe", 600)
+    kw = dict(mcmc=23, burnin=7, thin=4, chains=2, seed=4242)
+    full = _bi(df, **kw)
+    summ = _bi(df, draw_sink="summary", **kw)
+    nd = (23 - 1) // 4 + 1
+    assert full["level_1"][0].shape == (nd, 600, 4) and full["level_2"][0].shape == (nd, 5)
+    assert summ["level_1"] is None and summ["summary"]["n_draws"] == nd
+    for c in range(2):
+        l1 = full["level_1"][c]
+        np.testing.assert_allclose(summ["summary"]["lambda"][c], l1[:, :, 0].mean(0), rtol=1e-12)
+        np.testing.assert_allclose(summ["summary"]["z"][c], l1[:, :, 3].mean(0), rtol=1e-12, atol=1e-15)
+        np.testing.assert_allclose(summ["summary"]["log_mu"][c], np.log(l1[:, :, 1]).mean(0), rtol=1e-12)
+        assert np.array_equal(bits(summ["level_2"][c]), bits(full["level_2"][c]))
+
+
+def test_edge_cases(L):
+    """Single customer, zero-MH-step sweeps, all-zero repeat customers, maximum K=9/D=3."""
+    from mcmc_clv_model_amd import mcmc_draw_parameters, mcmc_draw_parameters_rfm_m
+    df = cdnow("abe")
+    one = df.iloc[:1].copy()
+    d = mcmc_draw_parameters(one, mcmc=5, burnin=2, thin=1, chains=1, seed=1, trace=0)
+    assert np.isfinite(d["level_1"][0]).all()
+    d = mcmc_draw_parameters(df.iloc[:300], mcmc=3, burnin=0, thin=1, chains=1, seed=1, trace=0, n_mh_steps=0)
+    assert np.isfinite(d["level_2"][0]).all()
+    zero = df[df["x"] == 0].iloc[:400].copy()
+    d = mcmc_draw_parameters(zero, mcmc=5, burnin=5, thin=1, chains=1, seed=2, trace=0)
+    assert np.isfinite(d["level_1"][0]).all()
+    rng = np.random.default_rng(0)
+    big = df.iloc[:800].copy()
+    covs = []
+    for k in range(8):
+        big[f"c{k}"] = rng.uniform(-1, 1, len(big))
+        covs.append(f"c{k}")
+    d = mcmc_draw_parameters_rfm_m(big, covs, mcmc=4, burnin=2, thin=1, chains=2, seed=3, trace=0)
+    assert d["level_2"][0].shape == (4, 3 * 9 + 6) and np.isfinite(d["level_2"][0]).all()
+    assert isinstance(d["log_likelihood"], float)
+
+
+def test_validation_errors_match_reference(L):
+    from mcmc_clv_model_amd import mcmc_draw_parameters
+    df = cdnow("abe", 10)
+    with pytest.raises(ValueError, match="cal_cbs missing required column 't_x'"):
+        mcmc_draw_parameters(df.drop(columns=["t_x"]))
+    with pytest.raises(ValueError, match="some covariate columns not in cal_cbs"):
+        mcmc_draw_parameters(df, ["nope"])
+
+
+def test_trace_lines(L, capsys):
+    df = cdnow("abe", 100)
+    _bi(df, mcmc=4, burnin=4, thin=1, chains=2, trace=4)
+    out = capsys.readouterr().out.splitlines()
+    assert out == ["chain 1 | step 4/8", "chain 2 | step 4/8", "chain 1 | step 8/8", "chain 2 | step 8/8"]
