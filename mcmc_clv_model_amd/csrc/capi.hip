@@ -58,6 +58,7 @@ struct clv_sampler {
   double *d_block = nullptr, *d_unit = nullptr;
   double* d_prior = nullptr;
   Ctrl* d_ctrl = nullptr;
+  uint32_t* d_arrive = nullptr;     // [chain] fused-tail arrival counters
   double *d_level1 = nullptr, *d_level2 = nullptr, *d_loglik = nullptr, *d_sums = nullptr;
   double* d_tape = nullptr;
   double* d_bs = nullptr;  // staging for set_hyper
@@ -78,7 +79,9 @@ struct clv_sampler {
 
 namespace {
 
-SweepArgs sweep_args(clv_sampler* s, int init) {
+HyperArgs hyper_args(clv_sampler* s, const double* units, int mode);
+
+SweepArgs sweep_args(clv_sampler* s, int init, int fuse = 0) {
   SweepArgs a{};
   a.g = s->g;
   a.r.seed = s->cfg.seed;
@@ -101,6 +104,9 @@ SweepArgs sweep_args(clv_sampler* s, int init) {
   a.n_stored = nullptr;
   a.lam_init = s->prior.lam_init;
   a.init = init;
+  a.fuse = fuse;
+  a.chain_arrive = s->d_arrive;
+  if (fuse) a.h = hyper_args(s, nullptr, 0);
   return a;
 }
 
@@ -141,6 +147,14 @@ int enqueue_sweep(clv_sampler* s, hipEvent_t e0, hipEvent_t e1) {
   return CLV_OK;
 }
 
+// world_size == 1: one launch per sweep (the level-2 draw runs in the sweep kernel's tail)
+int enqueue_fused(clv_sampler* s, hipEvent_t e0, hipEvent_t e1) {
+  if (e0) CLV_HIP(hipEventRecord(e0, s->stream));
+  CLV_HIP(launch_sweep(sweep_args(s, 0, 1), s->replay, s->stream));
+  if (e1) CLV_HIP(hipEventRecord(e1, s->stream));
+  return CLV_OK;
+}
+
 int enqueue_hyper(clv_sampler* s, const double* units, int mode, hipEvent_t e0, hipEvent_t e1) {
   if (e0) CLV_HIP(hipEventRecord(e0, s->stream));
   CLV_HIP(launch_hyper(hyper_args(s, units, mode), s->replay, s->stream));
@@ -159,15 +173,13 @@ int check_replay_range(clv_sampler* s, int64_t n_more) {
 
 int harvest_timing(clv_sampler* s) {
   if (s->ev_used == 0) return CLV_OK;
-  CLV_HIP(hipEventSynchronize(s->ev[4 * s->ev_used - 1]));
+  CLV_HIP(hipEventSynchronize(s->ev[4 * (s->ev_used - 1) + 1]));
   for (int k = 0; k < s->ev_used; ++k) {
     float ms = 0.f;
     CLV_HIP(hipEventElapsedTime(&ms, s->ev[4 * k], s->ev[4 * k + 1]));
     s->t_sweep_ms += ms;
     s->n_sweep_timed++;
-    CLV_HIP(hipEventElapsedTime(&ms, s->ev[4 * k + 2], s->ev[4 * k + 3]));
-    s->t_hyper_ms += ms;
-    s->n_hyper_timed++;
+    (void)0;  // fused: the level-2 draw is inside the timed sweep launch
   }
   s->ev_used = 0;
   return CLV_OK;
@@ -182,8 +194,7 @@ int build_graph(clv_sampler* s, int n) {
   hipGraph_t graph;
   CLV_HIP(hipStreamBeginCapture(s->stream, hipStreamCaptureModeThreadLocal));
   for (int k = 0; k < n; ++k) {
-    int rc = enqueue_sweep(s, nullptr, nullptr);
-    if (rc == CLV_OK) rc = enqueue_hyper(s, nullptr, 0, nullptr, nullptr);
+    int rc = enqueue_fused(s, nullptr, nullptr);
     if (rc != CLV_OK) {
       hipGraph_t dummy;
       (void)hipStreamEndCapture(s->stream, &dummy);
@@ -333,6 +344,8 @@ int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* pri
   else s->d_unit = s->d_block;
   CLV_HIPC(dalloc(&s->d_prior, PRIOR_DOUBLES));
   CLV_HIPC(dalloc(&s->d_ctrl, 1));
+  CLV_HIPC(dalloc(&s->d_arrive, C));
+  CLV_HIPC(hipMemsetAsync(s->d_arrive, 0, sizeof(uint32_t) * C, s->stream));
   CLV_HIPC(dalloc(&s->d_bs, C * (CLV_MAX_K * CLV_MAX_D + CLV_MAX_D * CLV_MAX_D)));
   if (g.n_draws > 0) {
     CLV_HIPC(dalloc(&s->d_level2, (size_t)C * g.n_draws * g.l2w));
@@ -412,7 +425,7 @@ void clv_destroy(clv_sampler* s) {
   for (auto e : s->ev) (void)hipEventDestroy(e);
   void* ptrs[] = {s->d_x, s->d_tx, s->d_T, s->d_cov, s->d_logs, s->d_lam, s->d_mu, s->d_hyper,
                   s->d_block, s->d_prior, s->d_ctrl, s->d_level1, s->d_level2, s->d_loglik,
-                  s->d_sums, s->d_tape, s->d_bs};
+                  s->d_sums, s->d_tape, s->d_bs, s->d_arrive};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (s->d_unit && s->d_unit != s->d_block) (void)hipFree(s->d_unit);
@@ -509,8 +522,7 @@ int clv_run(clv_sampler* s, int64_t n_sweeps) {
     }
     while (left > 0) {
       const int k = s->ev_used;
-      rc = enqueue_sweep(s, s->ev[4 * k], s->ev[4 * k + 1]);
-      if (rc == CLV_OK) rc = enqueue_hyper(s, nullptr, 0, s->ev[4 * k + 2], s->ev[4 * k + 3]);
+      rc = enqueue_fused(s, s->ev[4 * k], s->ev[4 * k + 1]);
       if (rc) return rc;
       s->ev_used++;
       s->sweeps_done++;
@@ -533,8 +545,7 @@ int clv_run(clv_sampler* s, int64_t n_sweeps) {
       }
     }
     while (left > 0) {
-      rc = enqueue_sweep(s, nullptr, nullptr);
-      if (rc == CLV_OK) rc = enqueue_hyper(s, nullptr, 0, nullptr, nullptr);
+      rc = enqueue_fused(s, nullptr, nullptr);
       if (rc) return rc;
       s->sweeps_done++;
       left--;

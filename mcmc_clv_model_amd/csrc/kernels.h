@@ -51,6 +51,23 @@ struct Rng {
   int64_t tape_sweeps;
 };
 
+struct HyperArgs {
+  Geometry g;
+  Rng r;
+  const double* units;       // [world][chain][units_per_rank][stride]
+  double* hyper;             // [chain][HS]
+  Ctrl* ctrl;
+  double* level2;            // [chain][n_draws][l2w]
+  double* loglik;            // [chain][n_draws]
+  const double* V;           // K x K
+  const double* cholV;       // K x K lower
+  const double* A0B0;        // K x D
+  const double* S0B;         // D x D: S0 + B0'A0B0
+  double nu_n;
+  double omega2;
+  int mode;                  // 0: after sweep (cur+1); 1: bivariate initial draw (sweep 1)
+};
+
 struct SweepArgs {
   Geometry g;
   Rng r;
@@ -69,6 +86,9 @@ struct SweepArgs {
   int64_t* n_stored;         // device counter of stored draws (chain 0 block 0 bumps it)
   double lam_init;
   int init;                  // 1: initialisation pass (bi:367-370), no sweep
+  int fuse;                  // 1: the chain's last-arriving workgroup performs the level-2 draw
+  uint32_t* chain_arrive;    // [chain] arrival counters of the fused tail (zero between launches)
+  HyperArgs h;               // level-2 arguments of the fused tail
 };
 
 struct GroupArgs {
@@ -77,22 +97,6 @@ struct GroupArgs {
   double* unitpart;          // [chain][units_per_rank][stride]
 };
 
-struct HyperArgs {
-  Geometry g;
-  Rng r;
-  const double* units;       // [world][chain][units_per_rank][stride]
-  double* hyper;             // [chain][HS]
-  Ctrl* ctrl;
-  double* level2;            // [chain][n_draws][l2w]
-  double* loglik;            // [chain][n_draws]
-  const double* V;           // K x K
-  const double* cholV;       // K x K lower
-  const double* A0B0;        // K x D
-  const double* S0B;         // D x D: S0 + B0'A0B0
-  double nu_n;
-  double omega2;
-  int mode;                  // 0: after sweep (cur+1); 1: bivariate initial draw (sweep 1)
-};
 
 // Launchers (kernels.hip).
 hipError_t launch_sweep(const SweepArgs& a, bool replay, hipStream_t st);

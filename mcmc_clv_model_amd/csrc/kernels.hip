@@ -74,6 +74,305 @@ __device__ __forceinline__ int64_t draw_index(int64_t s, const Geometry& g) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// Group kernel: unit partial = sequential sum of blocks_per_unit block partials.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void group_kernel(GroupArgs a) {
+  const Geometry& g = a.g;
+  const int u = blockIdx.x;
+  const int c = blockIdx.y;
+  const int j = threadIdx.x;
+  if (j >= g.stride) return;
+  const double* p = a.blockpart + ((int64_t)c * g.blocks_per_rank + (int64_t)u * g.blocks_per_unit) * g.stride + j;
+  double t = 0.0;
+  for (int bb = 0; bb < g.blocks_per_unit; ++bb) t += p[(int64_t)bb * g.stride];
+  a.unitpart[((int64_t)c * g.units_per_rank + u) * g.stride + j] = t;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Level-2 algebra (bi:243-261) on reduced statistics.
+// ---------------------------------------------------------------------------------------------
+template <int D>
+__device__ void cholesky(const double (&A)[D][D], double (&L)[D][D]) {
+#pragma unroll
+  for (int r = 0; r < D; ++r)
+#pragma unroll
+    for (int q = 0; q < D; ++q) L[r][q] = 0.0;
+#pragma unroll
+  for (int j = 0; j < D; ++j) {
+    double sdiag = A[j][j];
+#pragma unroll
+    for (int k = 0; k < j; ++k) sdiag -= L[j][k] * L[j][k];
+    L[j][j] = sqrt(sdiag);
+#pragma unroll
+    for (int r = j + 1; r < D; ++r) {
+      double sv = A[r][j];
+#pragma unroll
+      for (int k = 0; k < j; ++k) sv -= L[r][k] * L[j][k];
+      L[r][j] = sv / L[j][j];
+    }
+  }
+}
+
+// hyper-state finalisation from (beta, Sigma): inverse block, proposal scales, eta constants.
+template <int D, int K>
+__device__ void finalize_hyper(const double (&beta)[K][D], const double (&Sig)[D][D], double omega2, double* H) {
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+#pragma unroll
+    for (int d = 0; d < D; ++d) H[H_BETA + k * D + d] = beta[k][d];
+  for (int q = 0; q < 9; ++q) H[H_SIGMA + q] = 0.0;
+#pragma unroll
+  for (int p = 0; p < D; ++p)
+#pragma unroll
+    for (int q = 0; q < D; ++q) H[H_SIGMA + p * 3 + q] = Sig[p][q];
+  if constexpr (D == 2) {
+    const double det = Sig[0][0] * Sig[1][1] - Sig[0][1] * Sig[1][0];
+    H[H_P00] = Sig[1][1] / det;
+    H[H_P01] = -Sig[0][1] / det;
+    H[H_P11] = Sig[0][0] / det;
+  } else {
+    // top-left 2x2 block of the full 3x3 inverse (tri:402 with tri:422-424; quirk Q4)
+    const double c00 = Sig[1][1] * Sig[2][2] - Sig[1][2] * Sig[2][1];
+    const double c01 = Sig[1][0] * Sig[2][2] - Sig[1][2] * Sig[2][0];
+    const double c02 = Sig[1][0] * Sig[2][1] - Sig[1][1] * Sig[2][0];
+    const double det = Sig[0][0] * c00 - Sig[0][1] * c01 + Sig[0][2] * c02;
+    H[H_P00] = c00 / det;
+    H[H_P01] = -(Sig[0][1] * Sig[2][2] - Sig[0][2] * Sig[2][1]) / det;
+    H[H_P11] = (Sig[0][0] * Sig[2][2] - Sig[0][2] * Sig[2][0]) / det;
+    H[H_S22] = Sig[2][2];
+    const double post_var = 1.0 / (1.0 / omega2 + 1.0 / Sig[2][2]);  // tri:325-326
+    H[H_POSTVAR] = post_var;
+    H[H_SQRT_POSTVAR] = sqrt(post_var);
+    H[H_OMEGA2] = omega2;
+  }
+  H[H_S00] = Sig[0][0];
+  H[H_S11] = Sig[1][1];
+}
+
+// Given the reduced statistics and the variates, draw (beta, Sigma).
+// iwn: n_tril normals, chi2: D chi-square draws, noise: either the replayed mvn noise (w, D*K) or
+// standard normals z (D*K) mapped through kron(chol(Sigma), chol(V)).
+template <int D, int K>
+__device__ void level2_draw(const double* tot, const double* V, const double* cholV, const double* A0B0,
+                            const double* S0B, const double* iwn, const double* chi2, const double* noise,
+                            bool noise_is_w, double (&beta)[K][D], double (&Sig)[D][D]) {
+  constexpr int NXY = K * D;
+  double R[K][D], Bh[K][D];
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+#pragma unroll
+    for (int d = 0; d < D; ++d) R[k][d] = tot[k * D + d] + A0B0[k * D + d];
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      double sv = 0.0;
+#pragma unroll
+      for (int j = 0; j < K; ++j) sv += V[k * K + j] * R[j][d];
+      Bh[k][d] = sv;
+    }
+  // S_n = S0 + Y'Y + B0'A0B0 - R'B_hat   (== S0 + E'E + C'A0C, bi:253-255)
+  double Sn[D][D];
+  int t = NXY;
+#pragma unroll
+  for (int p = 0; p < D; ++p)
+#pragma unroll
+    for (int q = p; q < D; ++q) {
+      double rb = 0.0;
+#pragma unroll
+      for (int k = 0; k < K; ++k) rb += R[k][p] * Bh[k][q];
+      const double v = (S0B[p * D + q] + tot[t++]) - rb;
+      Sn[p][q] = v;
+      Sn[q][p] = v;
+    }
+  // Sigma ~ IW(nu_n, S_n): scipy invwishart Bartlett form, Sigma = (L A^-1)(L A^-1)'
+  double L[D][D], A[D][D], M[D][D];
+  cholesky<D>(Sn, L);
+#pragma unroll
+  for (int p = 0; p < D; ++p)
+#pragma unroll
+    for (int q = 0; q < D; ++q) A[p][q] = 0.0;
+  {
+    int n = 0;
+#pragma unroll
+    for (int p = 1; p < D; ++p)
+#pragma unroll
+      for (int q = 0; q < p; ++q) A[p][q] = iwn[n++];  // np.tril_indices(D, -1) order
+#pragma unroll
+    for (int p = 0; p < D; ++p) A[p][p] = sqrt(chi2[p]);
+  }
+#pragma unroll
+  for (int r = 0; r < D; ++r)
+#pragma unroll
+    for (int j = D - 1; j >= 0; --j) {
+      double sv = L[r][j];
+#pragma unroll
+      for (int k = j + 1; k < D; ++k) sv -= M[r][k] * A[k][j];
+      M[r][j] = sv / A[j][j];
+    }
+#pragma unroll
+  for (int p = 0; p < D; ++p)
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+      double sv = 0.0;
+#pragma unroll
+      for (int k = 0; k < D; ++k) sv += M[p][k] * M[q][k];
+      Sig[p][q] = sv;
+    }
+#pragma unroll
+  for (int p = 0; p < D; ++p)
+#pragma unroll
+    for (int q = p + 1; q < D; ++q) Sig[q][p] = Sig[p][q];
+  // beta | Sigma: MVN(B_hat.ravel(), kron(Sigma, V)) with the reference's row-major ravel (quirk Q1)
+  double w[D * K];
+  if (noise_is_w) {
+#pragma unroll
+    for (int q = 0; q < D * K; ++q) w[q] = noise[q];
+  } else {
+    double Ls[D][D];
+    cholesky<D>(Sig, Ls);
+#pragma unroll
+    for (int p = 0; p < D; ++p)
+#pragma unroll
+      for (int bq = 0; bq < K; ++bq) {
+        double sv = 0.0;
+#pragma unroll
+        for (int cc = 0; cc <= p; ++cc)
+#pragma unroll
+          for (int e = 0; e <= bq; ++e) sv += Ls[p][cc] * cholV[bq * K + e] * noise[cc * K + e];
+        w[p * K + bq] = sv;
+      }
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+#pragma unroll
+    for (int d = 0; d < D; ++d) beta[k][d] = Bh[k][d] + w[k * D + d];
+}
+
+// Philox-mode hyper variates (fp64).
+__device__ double hyper_normal(uint32_t k0, uint32_t k1, uint32_t slot, uint32_t sweep) {
+  const u32x4 r = hyper_block(k0, k1, slot, sweep);
+  return sqrt(-2.0 * log(u53_open0(r.x, r.y))) * cospi(2.0 * u53(r.z, r.w));
+}
+
+// Marsaglia–Tsang Gamma(alpha, 1), alpha >= 1; chi2(df) = 2 Gamma(df / 2).
+__device__ double chi2_draw(uint32_t k0, uint32_t k1, uint32_t sweep, int idx, double df) {
+  const double alpha = 0.5 * df;
+  const double dd = alpha - 1.0 / 3.0;
+  const double cc = 1.0 / sqrt(9.0 * dd);
+  for (int at = 0; at < GAMMA_MAX_ATTEMPTS; ++at) {
+    const uint32_t slot = HSLOT_GAMMA0 + (uint32_t)idx * HSLOT_GAMMA_STRIDE + 2u * at;
+    const double x = hyper_normal(k0, k1, slot, sweep);
+    const double t = cc * x;
+    if (t <= -1.0) continue;
+    const double v1 = t * (3.0 + t * (3.0 + t));  // (1 + t)^3 - 1
+    const u32x4 r2 = hyper_block(k0, k1, slot + 1u, sweep);
+    const double lu = log(u53_open0(r2.x, r2.y));
+    if (lu < 0.5 * x * x + dd * (3.0 * log1p(t) - v1)) return 2.0 * dd * (1.0 + v1);
+  }
+  return df;  // unreachable in practice (acceptance > 0.95 per attempt)
+}
+
+// Level-2 draw of chain c after sweep s (mode 0), or the bivariate initial draw (mode 1):
+// fixed-order sum of all unit partials, variates, algebra, hyper state, level-2 record and
+// log-likelihood, then the sweep-counter arrival.  Executed by one 256-thread workgroup: the
+// standalone hyper_kernel (sharded path) or the last-arriving sweep workgroup of the chain
+// (fused path).  `blocks` != nullptr: read block partials and form each unit's sum on the fly
+// with the exact order of group_kernel (so both paths are bitwise identical).
+template <int D, int K, bool REPLAY, int NS>
+__device__ void hyper_body(const HyperArgs& a, int c, int64_t s, int mode, const double* blocks,
+                           double (*red)[NS], double* tot, double* var_iw, double* var_chi, double* var_noise) {
+  constexpr int NTRIL = D * (D - 1) / 2;
+  const Geometry& g = a.g;
+  const int tid = threadIdx.x;
+  const int64_t hs = (D == 2) ? s + 1 : s;  // sweep the drawn (beta, Sigma) belongs to
+
+  // 1. fixed-order reduction over all units of all shards (independent of world size)
+  double acc[NS];
+#pragma unroll
+  for (int j = 0; j < NS; ++j) acc[j] = 0.0;
+  for (int64_t u = tid; u < g.n_units_global; u += 256) {
+    if (blocks) {  // world_size == 1: units formed from this chain's block partials
+      const double* p = blocks + ((int64_t)c * g.blocks_per_rank + u * g.blocks_per_unit) * g.stride;
+#pragma unroll
+      for (int j = 0; j < NS; ++j) {
+        double t = 0.0;
+        for (int bb = 0; bb < g.blocks_per_unit; ++bb) t += p[(int64_t)bb * g.stride + j];
+        acc[j] += t;
+      }
+    } else {
+      const int64_t r = u / g.units_per_rank;
+      const int64_t lu = u - r * g.units_per_rank;
+      const double* p = a.units + ((r * g.n_chains + c) * g.units_per_rank + lu) * g.stride;
+#pragma unroll
+      for (int j = 0; j < NS; ++j) acc[j] += p[j];
+    }
+  }
+  block_reduce<NS>(acc, red, tot);
+
+  // 2. variates
+  if constexpr (REPLAY) {
+    const double* tv = a.r.tape + ((int64_t)c * a.r.tape_sweeps + (hs - 1)) * a.r.tape_sweep_stride +
+                       (a.r.tape_sweep_stride - TAPE_HYPER);
+    if (tid < 3) var_iw[tid] = tv[tid];
+    if (tid < 3) var_chi[tid] = tv[3 + tid];
+    if (tid < D * K) var_noise[tid] = tv[6 + tid];
+  } else {
+    uint32_t k0, k1;
+    chain_key(a.r.seed, (int64_t)a.r.chain_first + c, &k0, &k1);
+    if (tid < NTRIL) var_iw[tid] = hyper_normal(k0, k1, HSLOT_NORMAL0 + tid, (uint32_t)hs);
+    if (tid >= 64 && tid < 64 + D * K)
+      var_noise[tid - 64] = hyper_normal(k0, k1, HSLOT_BETA_NORMAL0 + (tid - 64), (uint32_t)hs);
+    if (tid >= 128 && tid < 128 + D) {
+      const int q = tid - 128;
+      var_chi[q] = chi2_draw(k0, k1, (uint32_t)hs, q, a.nu_n - D + 1 + q);
+    }
+  }
+  __syncthreads();
+
+  // 3. algebra + outputs (one lane)
+  if (tid == 0) {
+    double beta[K][D], Sig[D][D];
+    level2_draw<D, K>(tot, a.V, a.cholV, a.A0B0, a.S0B, var_iw, var_chi, var_noise, REPLAY, beta, Sig);
+    finalize_hyper<D, K>(beta, Sig, a.omega2, a.hyper + (int64_t)c * HS);
+    if (hs >= 1 && is_stored(hs, g)) {
+      double* o = a.level2 + ((int64_t)c * g.n_draws + draw_index(hs, g)) * g.l2w;
+      int q = 0;
+#pragma unroll
+      for (int d = 0; d < D; ++d)
+#pragma unroll
+        for (int k = 0; k < K; ++k) o[q++] = beta[k][d];  // beta.T.ravel() (bi:411)
+#pragma unroll
+      for (int p = 0; p < D; ++p)
+#pragma unroll
+        for (int r = p; r < D; ++r) o[q++] = Sig[p][r];  // bi:412, tri:550-554
+    }
+    if (mode == 0 && is_stored(s, g))
+      a.loglik[(int64_t)c * g.n_draws + draw_index(s, g)] = tot[NS - 1] / (double)g.n_global;  // np.mean
+    if (mode == 0) {
+      // the last chain to finish advances the sweep counter (every workgroup of this launch has
+      // read it before arriving)
+      const uint32_t old = __hip_atomic_fetch_add(&a.ctrl->arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      if (old == (uint32_t)g.n_chains - 1) {
+        __hip_atomic_store(&a.ctrl->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&a.ctrl->cur, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+}
+
+template <int D, int K, bool REPLAY>
+__global__ __launch_bounds__(256) void hyper_kernel(HyperArgs a) {
+  constexpr int NS = K * D + D * (D + 1) / 2 + 1;
+  __shared__ double red[4][NS];
+  __shared__ double tot[NS];
+  __shared__ double var_iw[4], var_chi[4], var_noise[32];
+  const int64_t done = __hip_atomic_load(&a.ctrl->cur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int64_t s = a.mode == 1 ? 0 : done + 1;  // sweep whose statistics are reduced here
+  hyper_body<D, K, REPLAY, NS>(a, blockIdx.x, s, a.mode, nullptr, red, tot, var_iw, var_chi, var_noise);
+}
+
+// ---------------------------------------------------------------------------------------------
 // Sweep kernel
 // ---------------------------------------------------------------------------------------------
 template <int D, int K, bool REPLAY>
@@ -289,285 +588,30 @@ __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
   block_reduce<NS>(acc, red, tot);
   if (threadIdx.x < NS)
     a.blockpart[((int64_t)c * g.blocks_per_rank + b) * g.stride + threadIdx.x] = tot[threadIdx.x];
-}
 
-// ---------------------------------------------------------------------------------------------
-// Group kernel: unit partial = sequential sum of blocks_per_unit block partials.
-// ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void group_kernel(GroupArgs a) {
-  const Geometry& g = a.g;
-  const int u = blockIdx.x;
-  const int c = blockIdx.y;
-  const int j = threadIdx.x;
-  if (j >= g.stride) return;
-  const double* p = a.blockpart + ((int64_t)c * g.blocks_per_rank + (int64_t)u * g.blocks_per_unit) * g.stride + j;
-  double t = 0.0;
-  for (int bb = 0; bb < g.blocks_per_unit; ++bb) t += p[(int64_t)bb * g.stride];
-  a.unitpart[((int64_t)c * g.units_per_rank + u) * g.stride + j] = t;
-}
-
-// ---------------------------------------------------------------------------------------------
-// Level-2 algebra (bi:243-261) on reduced statistics.
-// ---------------------------------------------------------------------------------------------
-template <int D>
-__device__ void cholesky(const double (&A)[D][D], double (&L)[D][D]) {
-#pragma unroll
-  for (int r = 0; r < D; ++r)
-#pragma unroll
-    for (int q = 0; q < D; ++q) L[r][q] = 0.0;
-#pragma unroll
-  for (int j = 0; j < D; ++j) {
-    double sdiag = A[j][j];
-#pragma unroll
-    for (int k = 0; k < j; ++k) sdiag -= L[j][k] * L[j][k];
-    L[j][j] = sqrt(sdiag);
-#pragma unroll
-    for (int r = j + 1; r < D; ++r) {
-      double sv = A[r][j];
-#pragma unroll
-      for (int k = 0; k < j; ++k) sv -= L[r][k] * L[j][k];
-      L[r][j] = sv / L[j][j];
-    }
-  }
-}
-
-// hyper-state finalisation from (beta, Sigma): inverse block, proposal scales, eta constants.
-template <int D, int K>
-__device__ void finalize_hyper(const double (&beta)[K][D], const double (&Sig)[D][D], double omega2, double* H) {
-#pragma unroll
-  for (int k = 0; k < K; ++k)
-#pragma unroll
-    for (int d = 0; d < D; ++d) H[H_BETA + k * D + d] = beta[k][d];
-  for (int q = 0; q < 9; ++q) H[H_SIGMA + q] = 0.0;
-#pragma unroll
-  for (int p = 0; p < D; ++p)
-#pragma unroll
-    for (int q = 0; q < D; ++q) H[H_SIGMA + p * 3 + q] = Sig[p][q];
-  if constexpr (D == 2) {
-    const double det = Sig[0][0] * Sig[1][1] - Sig[0][1] * Sig[1][0];
-    H[H_P00] = Sig[1][1] / det;
-    H[H_P01] = -Sig[0][1] / det;
-    H[H_P11] = Sig[0][0] / det;
-  } else {
-    // top-left 2x2 block of the full 3x3 inverse (tri:402 with tri:422-424; quirk Q4)
-    const double c00 = Sig[1][1] * Sig[2][2] - Sig[1][2] * Sig[2][1];
-    const double c01 = Sig[1][0] * Sig[2][2] - Sig[1][2] * Sig[2][0];
-    const double c02 = Sig[1][0] * Sig[2][1] - Sig[1][1] * Sig[2][0];
-    const double det = Sig[0][0] * c00 - Sig[0][1] * c01 + Sig[0][2] * c02;
-    H[H_P00] = c00 / det;
-    H[H_P01] = -(Sig[0][1] * Sig[2][2] - Sig[0][2] * Sig[2][1]) / det;
-    H[H_P11] = (Sig[0][0] * Sig[2][2] - Sig[0][2] * Sig[2][0]) / det;
-    H[H_S22] = Sig[2][2];
-    const double post_var = 1.0 / (1.0 / omega2 + 1.0 / Sig[2][2]);  // tri:325-326
-    H[H_POSTVAR] = post_var;
-    H[H_SQRT_POSTVAR] = sqrt(post_var);
-    H[H_OMEGA2] = omega2;
-  }
-  H[H_S00] = Sig[0][0];
-  H[H_S11] = Sig[1][1];
-}
-
-// Given the reduced statistics and the variates, draw (beta, Sigma).
-// iwn: n_tril normals, chi2: D chi-square draws, noise: either the replayed mvn noise (w, D*K) or
-// standard normals z (D*K) mapped through kron(chol(Sigma), chol(V)).
-template <int D, int K>
-__device__ void level2_draw(const double* tot, const double* V, const double* cholV, const double* A0B0,
-                            const double* S0B, const double* iwn, const double* chi2, const double* noise,
-                            bool noise_is_w, double (&beta)[K][D], double (&Sig)[D][D]) {
-  constexpr int NXY = K * D;
-  double R[K][D], Bh[K][D];
-#pragma unroll
-  for (int k = 0; k < K; ++k)
-#pragma unroll
-    for (int d = 0; d < D; ++d) R[k][d] = tot[k * D + d] + A0B0[k * D + d];
-#pragma unroll
-  for (int k = 0; k < K; ++k)
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-      double sv = 0.0;
-#pragma unroll
-      for (int j = 0; j < K; ++j) sv += V[k * K + j] * R[j][d];
-      Bh[k][d] = sv;
-    }
-  // S_n = S0 + Y'Y + B0'A0B0 - R'B_hat   (== S0 + E'E + C'A0C, bi:253-255)
-  double Sn[D][D];
-  int t = NXY;
-#pragma unroll
-  for (int p = 0; p < D; ++p)
-#pragma unroll
-    for (int q = p; q < D; ++q) {
-      double rb = 0.0;
-#pragma unroll
-      for (int k = 0; k < K; ++k) rb += R[k][p] * Bh[k][q];
-      const double v = (S0B[p * D + q] + tot[t++]) - rb;
-      Sn[p][q] = v;
-      Sn[q][p] = v;
-    }
-  // Sigma ~ IW(nu_n, S_n): scipy invwishart Bartlett form, Sigma = (L A^-1)(L A^-1)'
-  double L[D][D], A[D][D], M[D][D];
-  cholesky<D>(Sn, L);
-#pragma unroll
-  for (int p = 0; p < D; ++p)
-#pragma unroll
-    for (int q = 0; q < D; ++q) A[p][q] = 0.0;
-  {
-    int n = 0;
-#pragma unroll
-    for (int p = 1; p < D; ++p)
-#pragma unroll
-      for (int q = 0; q < p; ++q) A[p][q] = iwn[n++];  // np.tril_indices(D, -1) order
-#pragma unroll
-    for (int p = 0; p < D; ++p) A[p][p] = sqrt(chi2[p]);
-  }
-#pragma unroll
-  for (int r = 0; r < D; ++r)
-#pragma unroll
-    for (int j = D - 1; j >= 0; --j) {
-      double sv = L[r][j];
-#pragma unroll
-      for (int k = j + 1; k < D; ++k) sv -= M[r][k] * A[k][j];
-      M[r][j] = sv / A[j][j];
-    }
-#pragma unroll
-  for (int p = 0; p < D; ++p)
-#pragma unroll
-    for (int q = 0; q < D; ++q) {
-      double sv = 0.0;
-#pragma unroll
-      for (int k = 0; k < D; ++k) sv += M[p][k] * M[q][k];
-      Sig[p][q] = sv;
-    }
-#pragma unroll
-  for (int p = 0; p < D; ++p)
-#pragma unroll
-    for (int q = p + 1; q < D; ++q) Sig[q][p] = Sig[p][q];
-  // beta | Sigma: MVN(B_hat.ravel(), kron(Sigma, V)) with the reference's row-major ravel (quirk Q1)
-  double w[D * K];
-  if (noise_is_w) {
-#pragma unroll
-    for (int q = 0; q < D * K; ++q) w[q] = noise[q];
-  } else {
-    double Ls[D][D];
-    cholesky<D>(Sig, Ls);
-#pragma unroll
-    for (int p = 0; p < D; ++p)
-#pragma unroll
-      for (int bq = 0; bq < K; ++bq) {
-        double sv = 0.0;
-#pragma unroll
-        for (int cc = 0; cc <= p; ++cc)
-#pragma unroll
-          for (int e = 0; e <= bq; ++e) sv += Ls[p][cc] * cholV[bq * K + e] * noise[cc * K + e];
-        w[p * K + bq] = sv;
+  // ---- fused level-2 draw (world_size == 1): the chain's last workgroup to arrive reduces all
+  // block partials and draws (beta, Sigma) — no separate hyper launch per sweep.  Hand-off per
+  // MI355X guide Guideline 16: stores drained, agent release, atomic ticket; the last arriver
+  // takes an agent acquire before reading the other workgroups' partials.
+  if (a.fuse) {
+    __shared__ uint32_t s_last;
+    __shared__ double var_iw[4], var_chi[4], var_noise[32];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint32_t old = __hip_atomic_fetch_add(a.chain_arrive + c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t last = old == (uint32_t)(g.nb_local - 1) ? 1u : 0u;
+      if (last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(a.chain_arrive + c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-  }
-#pragma unroll
-  for (int k = 0; k < K; ++k)
-#pragma unroll
-    for (int d = 0; d < D; ++d) beta[k][d] = Bh[k][d] + w[k * D + d];
-}
-
-// Philox-mode hyper variates (fp64).
-__device__ double hyper_normal(uint32_t k0, uint32_t k1, uint32_t slot, uint32_t sweep) {
-  const u32x4 r = hyper_block(k0, k1, slot, sweep);
-  return sqrt(-2.0 * log(u53_open0(r.x, r.y))) * cospi(2.0 * u53(r.z, r.w));
-}
-
-// Marsaglia–Tsang Gamma(alpha, 1), alpha >= 1; chi2(df) = 2 Gamma(df / 2).
-__device__ double chi2_draw(uint32_t k0, uint32_t k1, uint32_t sweep, int idx, double df) {
-  const double alpha = 0.5 * df;
-  const double dd = alpha - 1.0 / 3.0;
-  const double cc = 1.0 / sqrt(9.0 * dd);
-  for (int at = 0; at < GAMMA_MAX_ATTEMPTS; ++at) {
-    const uint32_t slot = HSLOT_GAMMA0 + (uint32_t)idx * HSLOT_GAMMA_STRIDE + 2u * at;
-    const double x = hyper_normal(k0, k1, slot, sweep);
-    const double t = cc * x;
-    if (t <= -1.0) continue;
-    const double v1 = t * (3.0 + t * (3.0 + t));  // (1 + t)^3 - 1
-    const u32x4 r2 = hyper_block(k0, k1, slot + 1u, sweep);
-    const double lu = log(u53_open0(r2.x, r2.y));
-    if (lu < 0.5 * x * x + dd * (3.0 * log1p(t) - v1)) return 2.0 * dd * (1.0 + v1);
-  }
-  return df;  // unreachable in practice (acceptance > 0.95 per attempt)
-}
-
-template <int D, int K, bool REPLAY>
-__global__ __launch_bounds__(256) void hyper_kernel(HyperArgs a) {
-  constexpr int NXY = K * D;
-  constexpr int NYY = D * (D + 1) / 2;
-  constexpr int NS = NXY + NYY + 1;
-  constexpr int NTRIL = D * (D - 1) / 2;
-  __shared__ double red[4][NS];
-  __shared__ double tot[NS];
-  __shared__ double var_iw[4], var_chi[4], var_noise[32];
-
-  const Geometry& g = a.g;
-  const int c = blockIdx.x;
-  const int tid = threadIdx.x;
-  const int64_t done = __hip_atomic_load(&a.ctrl->cur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const int64_t s = a.mode == 1 ? 0 : done + 1;  // sweep whose statistics are reduced here
-  const int64_t hs = (D == 2) ? s + 1 : s;        // sweep the drawn (beta, Sigma) belongs to
-
-  // 1. fixed-order reduction over all units of all shards (independent of world size)
-  double acc[NS];
-#pragma unroll
-  for (int j = 0; j < NS; ++j) acc[j] = 0.0;
-  for (int64_t u = tid; u < g.n_units_global; u += 256) {
-    const int64_t r = u / g.units_per_rank;
-    const int64_t lu = u - r * g.units_per_rank;
-    const double* p = a.units + ((r * g.n_chains + c) * g.units_per_rank + lu) * g.stride;
-#pragma unroll
-    for (int j = 0; j < NS; ++j) acc[j] += p[j];
-  }
-  block_reduce<NS>(acc, red, tot);
-
-  // 2. variates
-  if constexpr (REPLAY) {
-    const double* tv = a.r.tape + ((int64_t)c * a.r.tape_sweeps + (hs - 1)) * a.r.tape_sweep_stride +
-                       (a.r.tape_sweep_stride - TAPE_HYPER);
-    if (tid < 3) var_iw[tid] = tv[tid];
-    if (tid < 3) var_chi[tid] = tv[3 + tid];
-    if (tid < D * K) var_noise[tid] = tv[6 + tid];
-  } else {
-    uint32_t k0, k1;
-    chain_key(a.r.seed, (int64_t)a.r.chain_first + c, &k0, &k1);
-    if (tid < NTRIL) var_iw[tid] = hyper_normal(k0, k1, HSLOT_NORMAL0 + tid, (uint32_t)hs);
-    if (tid >= 64 && tid < 64 + D * K)
-      var_noise[tid - 64] = hyper_normal(k0, k1, HSLOT_BETA_NORMAL0 + (tid - 64), (uint32_t)hs);
-    if (tid >= 128 && tid < 128 + D) {
-      const int q = tid - 128;
-      var_chi[q] = chi2_draw(k0, k1, (uint32_t)hs, q, a.nu_n - D + 1 + q);
+      s_last = last;
     }
-  }
-  __syncthreads();
-
-  // 3. algebra + outputs (one lane)
-  if (tid == 0) {
-    double beta[K][D], Sig[D][D];
-    level2_draw<D, K>(tot, a.V, a.cholV, a.A0B0, a.S0B, var_iw, var_chi, var_noise, REPLAY, beta, Sig);
-    finalize_hyper<D, K>(beta, Sig, a.omega2, a.hyper + (int64_t)c * HS);
-    if (hs >= 1 && is_stored(hs, g)) {
-      double* o = a.level2 + ((int64_t)c * g.n_draws + draw_index(hs, g)) * g.l2w;
-      int q = 0;
-#pragma unroll
-      for (int d = 0; d < D; ++d)
-#pragma unroll
-        for (int k = 0; k < K; ++k) o[q++] = beta[k][d];  // beta.T.ravel() (bi:411)
-#pragma unroll
-      for (int p = 0; p < D; ++p)
-#pragma unroll
-        for (int r = p; r < D; ++r) o[q++] = Sig[p][r];  // bi:412, tri:550-554
-    }
-    if (a.mode == 0 && is_stored(s, g))
-      a.loglik[(int64_t)c * g.n_draws + draw_index(s, g)] = tot[NS - 1] / (double)g.n_global;  // np.mean
-    if (a.mode == 0) {
-      __atomic_signal_fence(__ATOMIC_SEQ_CST);
-      const uint32_t old = __hip_atomic_fetch_add(&a.ctrl->arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-      if (old == (uint32_t)g.n_chains - 1) {
-        __hip_atomic_store(&a.ctrl->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&a.ctrl->cur, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
+    __syncthreads();
+    if (s_last) hyper_body<D, K, REPLAY, NS>(a.h, c, s, 0, a.blockpart, red, tot, var_iw, var_chi, var_noise);
   }
 }
 

@@ -309,11 +309,11 @@ def _envelope_chain(args):
     return st, np.median(d["level_2"][0], axis=0), float(d["log_likelihood"])
 
 
-def write_envelope(M=8, burnin=2000, mcmc=2000):
+def write_envelope(M=16, burnin=2000, mcmc=2000):
     cases = [("c1_bi_k1", "bi", []), ("abe_bi_k2", "bi", ["first_sales_scaled"]),
              ("abe_tri_k3", "tri", ["gender_F", "age_scaled"])]
     jobs = [(kind, covs, 1000 + m, burnin, mcmc) for _, kind, covs in cases for m in range(M)]
-    with Pool(min(8, len(jobs))) as pool:
+    with Pool(min(8, len(jobs))) as pool:  # 1 thread per process
         res = pool.map(_envelope_chain, jobs)
     for ci, (name, kind, covs) in enumerate(cases):
         rs = res[ci * M:(ci + 1) * M]

@@ -1,0 +1,98 @@
+"""GPU statistical parity of the Philox-mode sampler with the reference.
+
+The reference's PCG64 stream cannot be reproduced by a parallel counter-based RNG, so parity in
+production mode is distributional: the fixtures hold per-customer posterior
+summaries of M = 8 independent chains of the reference (oracle, bitwise equal to it), and the
+GPU's M chains must agree within Monte-Carlo tolerance.  The published Table 3 (config 1) is a
+second, looser pin.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+from scipy.special import gammaln
+
+from tests.helpers import GOLDEN, cdnow, golden
+
+pytestmark = pytest.mark.gpu
+
+SD_FLOOR = dict(log_lambda=1e-3, log_mu=1e-3, p_alive=2e-3, lam=1e-5, log_eta=1e-3)
+
+
+def _run_envelope(name, M=16, seed=777):
+    from mcmc_clv_model_amd import mcmc_draw_parameters, mcmc_draw_parameters_rfm_m
+    f = golden(f"envelope_{name}.npz")
+    covs = [str(c) for c in f["covariates"]]
+    fn = mcmc_draw_parameters if str(f["kind"]) == "bi" else mcmc_draw_parameters_rfm_m
+    d = fn(cdnow("abe"), covs, mcmc=int(f["mcmc"]), burnin=int(f["burnin"]), thin=1, chains=M, seed=seed, trace=0)
+    stats = dict(log_lambda=[], log_mu=[], p_alive=[], lam=[], log_eta=[])
+    for l1 in d["level_1"]:
+        stats["log_lambda"].append(np.log(l1[:, :, 0]).mean(0))
+        stats["log_mu"].append(np.log(l1[:, :, 1]).mean(0))
+        stats["p_alive"].append(l1[:, :, 3].mean(0))
+        stats["lam"].append(l1[:, :, 0].mean(0))
+        if l1.shape[2] == 5:
+            stats["log_eta"].append(np.log(l1[:, :, 4]).mean(0))
+    return f, {k: np.stack(v) for k, v in stats.items() if v}, d
+
+
+@pytest.mark.parametrize("name", ["c1_bi_k1", "abe_bi_k2", "abe_tri_k3"])
+def test_posterior_envelope_vs_reference_ensemble(name):
+    """Per customer: |mean_gpu - mean_ref| <= 4 * sqrt(sd_ref^2/M + sd_gpu^2/M) for >= 99% of
+    customers; population means within 4 standard errors; per level-2 parameter, the mean of the
+    chains' posterior medians differs by <= 4.5 two-sample standard errors (M = 16 vs 16 chains).
+    Calibration: two independent 8-chain ensembles of the reference itself differ by up to
+    |z| = 2.8 on Sigma01/Sigma11, which mix slowly at 2000 + 2000 sweeps."""
+    f, g, d = _run_envelope(name)
+    M_ref = int(f["M"])
+    for k, v in g.items():
+        M = v.shape[0]
+        m_g, s_g = v.mean(0), v.std(0, ddof=1)
+        m_r, s_r = f[k + "_mean"], f[k + "_sd"]
+        se = np.sqrt(np.maximum(s_r, SD_FLOOR[k]) ** 2 / M_ref + np.maximum(s_g, SD_FLOOR[k]) ** 2 / M)
+        z = (m_g - m_r) / se
+        frac = np.mean(np.abs(z) <= 4.0)
+        assert frac >= 0.99, f"{name}/{k}: only {frac:.4f} of customers within 4 sigma"
+        pop_r = f[k + "_chains"]
+        pop_g = v.mean(1)
+        se_pop = np.sqrt(pop_r.var(ddof=1) / M_ref + pop_g.var(ddof=1) / M)
+        assert abs(pop_g.mean() - pop_r.mean()) <= 4 * se_pop + 1e-12, (k, pop_g.mean(), pop_r.mean(), se_pop)
+    med_g = np.median(np.stack(d["level_2"]), axis=1)      # (M, n_params) chain medians
+    med_r = f["level2_median"]
+    se = np.sqrt(med_g.var(0, ddof=1) / len(med_g) + med_r.var(0, ddof=1) / len(med_r))
+    z = (med_g.mean(0) - med_r.mean(0)) / np.maximum(se, 1e-12)
+    assert np.all(np.abs(z) <= 4.5), (np.abs(z).round(2), med_g.mean(0), med_r.mean(0))
+
+
+def _table3():
+    t = json.load(open(os.path.join(GOLDEN, "published_table3.json")))["Table 3"]
+    rows = {r.get("A"): r for r in t}
+    q = lambda label: [rows[label][c] for c in ("B", "C", "D")]  # noqa: E731  (HB M1 column)
+    return dict(beta_l0=q("Purchase rate log(λ) - Intercept"), beta_m0=q("Dropout rate log(μ) - Intercept"),
+                s00=q("sigma^2_λ = var[log λ]"),
+                s01=q("sigma^2_μ = var[log μ]"),      # mislabelled in the sheet: column holds Sigma01
+                s11=q("sigma_λ_μ = cov[log λ, log μ]"),  # ... and this one Sigma11
+                corr=q("Correlation computed from Γ₀"), loglik=rows["Marginal log-likelihood"]["C"])
+
+
+def test_published_table3_config1():
+    """Config 1 exactly as run_mcmc_abe.py:61-71 (M1, 4 chains, burnin 10000, 4000 draws, seed 42).
+    Chain-0 level-2 quantiles (analysis_abe.py:146) vs abe_replication.xlsx Table 3 "HB M1": each
+    of our medians lies inside the published 95% interval and each published median inside ours;
+    the marginal log-likelihood (chain_total_loglik, analysis_bi_helpers.py:52-72) within 1%."""
+    from mcmc_clv_model_amd import mcmc_draw_parameters
+    cbs = cdnow("abe")
+    d = mcmc_draw_parameters(cbs, [], mcmc=4000, burnin=10000, thin=1, chains=4, seed=42, trace=0)
+    l2 = d["level_2"][0]
+    corr = l2[:, -2] / np.sqrt(l2[:, -3] * l2[:, -1])
+    ours = dict(beta_l0=l2[:, 0], beta_m0=l2[:, 1], s00=l2[:, 2], s01=l2[:, 3], s11=l2[:, 4], corr=corr)
+    pub = _table3()
+    for k, v in ours.items():
+        q = np.percentile(v, [2.5, 50, 97.5])
+        p = pub[k]
+        assert p[0] <= q[1] <= p[2], (k, q, p)
+        assert q[0] <= p[1] <= q[2], (k, q, p)
+    x = cbs["x"].to_numpy()
+    total_loglik = float(d["log_likelihood"]) * len(cbs) - gammaln(x + 1).sum()
+    assert abs(total_loglik - pub["loglik"]) <= 0.01 * abs(pub["loglik"]), (total_loglik, pub["loglik"])

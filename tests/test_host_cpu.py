@@ -1,0 +1,198 @@
+"""CPU: the C-ABI library loads and exports every declared symbol; host-side setup is
+bit-identical to the reference's; the product fails loudly without a GPU; the sharded exchange
+(world_size 2, gloo) reproduces the single-process fixed-order reduction bit for bit."""
+import ctypes
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from oracle import ref_cpu as orc
+from tests.helpers import bits, cdnow
+
+
+def test_library_loads_and_exports_header_symbols():
+    from mcmc_clv_model_amd import _lib
+    L = _lib.lib()
+    names = _lib.exported_symbols()
+    assert len(names) >= 25
+    for n in names:
+        assert hasattr(L, n), f"{n} declared in include/clvmcmc.h but not exported"
+    assert L.clv_abi_version() == _lib.ABI_VERSION
+    for i, st in enumerate((_lib.ClvConfig, _lib.ClvData, _lib.ClvPrior)):
+        assert L.clv_sizeof(i) == ctypes.sizeof(st)
+
+
+def test_default_blocks_per_unit_matches_python_plan():
+    from mcmc_clv_model_amd import _lib
+    from mcmc_clv_model_amd.distributed import default_blocks_per_unit
+    L = _lib.lib()
+    for n in (1, 255, 256, 2357, 23570, 131072, 131073, 1_000_000, 10_000_000, 4_000_000_000):
+        assert L.clv_default_blocks_per_unit(n) == default_blocks_per_unit(n)
+
+
+@pytest.mark.parametrize("D,covs", [(2, []), (2, ["first_sales_scaled"]), (3, ["gender_F", "age_scaled"])])
+def test_host_setup_is_reference_identical(D, covs):
+    """Constants handed to the device = what the reference computes (bi:367-379, 467-479, 248-249)."""
+    from mcmc_clv_model_amd.sampler import build_problem, make_prior
+    df = cdnow("abe")
+    p = build_problem(df, covs, D)
+    cbs, X = orc.design_matrix(df, covs)
+    lam_init, lambdas, mus = orc.init_state(cbs["x"].to_numpy(), cbs["t_x"].to_numpy(), cbs["T_cal"].to_numpy())
+    assert bits(p.lam_init) == bits(lam_init)
+    hyper = orc.default_hyper(X.shape[1], D)
+    V, *_ = orc.level2_posterior(X, np.zeros((len(df), D)), hyper)
+    assert np.array_equal(bits(p.V), bits(V))
+    assert p.beta_0[0, 0] == np.log(lambdas.mean()) and p.beta_0[0, 1] == np.log(mus.mean())
+    if D == 3:
+        assert p.omega2 == cbs["log_s"].var() and p.beta_0[0, 2] == cbs["log_s"].mean()
+    pr = make_prior(p)
+    assert pr.nu_n == hyper["nu_00"] + len(df)
+    assert np.array_equal(p.cov, X[:, 1:].T)
+
+
+def test_validation_errors_before_device():
+    from mcmc_clv_model_amd import mcmc_draw_parameters
+    df = cdnow("abe", 10)
+    with pytest.raises(ValueError, match="cal_cbs missing required column 'x'"):
+        mcmc_draw_parameters(df.drop(columns=["x"]))
+    with pytest.raises(ValueError, match="some covariate columns not in cal_cbs"):
+        mcmc_draw_parameters(df, ["nope"])
+
+
+def test_no_cpu_fallback_without_gpu():
+    """The product path raises instead of silently running on the CPU."""
+    from mcmc_clv_model_amd import _lib, mcmc_draw_parameters
+    if _lib.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    with pytest.raises(_lib.ClvError, match="no HIP device"):
+        mcmc_draw_parameters(cdnow("abe", 100), mcmc=2, burnin=0, thin=1, chains=1, seed=1, trace=0)
+
+
+def test_c_abi_rejects_bad_configs():
+    """Argument checks in clv_create run before any device call."""
+    from mcmc_clv_model_amd import _lib
+    from mcmc_clv_model_amd.sampler import build_problem, make_prior
+    L = _lib.lib()
+    p = build_problem(cdnow("abe", 300), [], 2)
+    base = dict(abi_version=1, D=2, K=1, n_mh_steps=20, burnin=0, mcmc=2, thin=1, n_chains=1, chain_first=0,
+                rng_mode=0, draw_sink=0, device=-1, seed=1, n_global=300, shard_begin=0, world_size=1, rank=0,
+                blocks_per_rank=0, blocks_per_unit=0, stream=0)
+    data = _lib.ClvData(n=300, x=p.x.ctypes.data, t_x=p.t_x.ctypes.data, T_cal=p.T_cal.ctypes.data)
+    pr = make_prior(p)
+    for bad in (dict(D=4), dict(K=10), dict(thin=0), dict(n_chains=0), dict(abi_version=2), dict(blocks_per_unit=3),
+                dict(world_size=2, rank=0, blocks_per_rank=0), dict(rng_mode=1, world_size=2, blocks_per_rank=2),
+                dict(n_global=299), dict(shard_begin=256)):
+        cfg = _lib.ClvConfig(**dict(base, **bad))
+        h = ctypes.c_void_p()
+        rc = L.clv_create(ctypes.byref(cfg), ctypes.byref(data), ctypes.byref(pr), ctypes.byref(h))
+        assert rc == -1, (bad, rc)
+        assert L.clv_last_error()
+
+
+# ---------------------------------------------------------------------------------------------
+# Sharded exchange on CPU (gloo): plan + all_gather layout + the hyper kernel's fixed-order sum.
+def fixed_order_sum(units: np.ndarray, n_units_global: int, upr: int, world: int, chain: int, n_chains: int):
+    """numpy restatement of hyper_kernel's reduction order (kernels.hip): thread t of 256 sums
+    units t, t+256, ... sequentially; each 64-lane wave combines lanes by an xor butterfly; lane 0
+    of the 4 waves are added in wave order."""
+    stride = units.shape[-1]
+    acc = np.zeros((256, stride))
+    for t in range(256):
+        for u in range(t, n_units_global, 256):
+            r, lu = divmod(u, upr)
+            acc[t] += units[r, chain, lu]
+    waves = []
+    for w in range(4):
+        v = acc[64 * w:64 * (w + 1)].copy()
+        for off in (32, 16, 8, 4, 2, 1):
+            v = v + v[np.arange(64) ^ off]
+        waves.append(v[0])
+    return ((waves[0] + waves[1]) + waves[2]) + waves[3]
+
+
+def _unit_partials(stats_per_customer: np.ndarray, begin: int, end: int, plan, n_chains: int):
+    """Block partials (sum of 256 customers, butterfly order irrelevant here: shard-local and
+    identical on every rank layout) grouped into units, as the device lays them out."""
+    stride = stats_per_customer.shape[-1]
+    bpr, G = plan.blocks_per_rank, plan.blocks_per_unit
+    blocks = np.zeros((n_chains, bpr, stride))
+    for b in range(bpr):
+        lo, hi = begin + b * 256, min(end, begin + (b + 1) * 256)
+        if lo < hi:
+            blocks[:, b] = stats_per_customer[:, lo:hi].sum(1)
+    units = np.zeros((n_chains, bpr // G, stride))
+    for u in range(bpr // G):
+        for bb in range(G):
+            units[:, u] += blocks[:, u * G + bb]
+    return units
+
+
+def _worker(rank, world, port, n_global, q):
+    import torch
+    import torch.distributed as dist
+    from mcmc_clv_model_amd import distributed as D
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.default_rng(0)
+    C, stride = 2, 5
+    stats = rng.normal(size=(C, n_global, stride))
+    plan = D.plan(n_global, world)
+    b, e = plan.shard(rank)
+    units = _unit_partials(stats, b, e, plan, C)
+    local = torch.from_numpy(units.reshape(-1).copy())
+    gathered = torch.zeros(local.numel() * world, dtype=torch.float64)
+    D.exchange(local, gathered)
+    g = gathered.numpy().reshape(world, C, plan.units_per_rank, stride)
+    sums = [fixed_order_sum(g, plan.n_units_global, plan.units_per_rank, world, c, C) for c in range(C)]
+    q.put((rank, np.stack(sums), (b, e)))
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("n_global", [23570, 140_000])
+def test_sharded_exchange_world2_gloo_matches_single_process(n_global):
+    import multiprocessing as mp
+    from mcmc_clv_model_amd import distributed as D
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, n_global, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in procs], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # single-process reference: world 1
+    rng = np.random.default_rng(0)
+    stats = rng.normal(size=(2, n_global, 5))
+    plan1 = D.plan(n_global, 1)
+    u1 = _unit_partials(stats, 0, n_global, plan1, 2)[None]
+    ref = np.stack([fixed_order_sum(u1, plan1.n_units_global, plan1.units_per_rank, 1, c, 2) for c in range(2)])
+    (_, s0, (b0, e0)), (_, s1, (b1, e1)) = res
+    assert b0 == 0 and e0 == b1 and e1 == n_global           # contiguous cover
+    assert b1 % (256 * D.plan(n_global, 2).blocks_per_unit) == 0
+    assert np.array_equal(bits(s0), bits(s1))                 # every rank draws identically
+    assert np.array_equal(bits(s0), bits(ref))                # ... and equal to 1 GPU, bit for bit
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_shard_plan_covers_and_aligns(world):
+    from mcmc_clv_model_amd import distributed as D
+    for n in (1, 300, 23570, 1_000_000, 10_000_000):
+        p = D.plan(n, world)
+        spans = [p.shard(r) for r in range(world)]
+        assert spans[0][0] == 0 and spans[-1][1] == n
+        assert all(spans[r][1] == spans[r + 1][0] for r in range(world - 1))
+        assert p.blocks_per_rank % p.blocks_per_unit == 0
+        assert p.blocks_per_unit == D.default_blocks_per_unit(n)  # world-independent unit size
+        assert p.units_per_rank * world >= p.n_units_global
