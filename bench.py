@@ -9,9 +9,12 @@ weak scaling: every rank holds one 23,570-customer CDNOW copy of a N x 23,570-cu
 and the ranks exchange the level-2 sufficient statistics once per sweep over RCCL.
 
 Prints ONE JSON line (rank 0).  value = chains * customers * steps / wall time of the timed
-region (max over ranks).  roofline: the sweep kernel's algorithmic bytes per launch / its mean
-launch time from HIP events recorded around every launch of the timed region.  cpu_baseline:
-the bitwise-pinned numpy restatement of the reference (oracle/ref_cpu.py) on 1 core.
+region (hipGraph replay of the fused sweep launches; max over ranks).  roofline: the sweep
+kernel's algorithmic bytes per launch / its mean launch duration, measured with HIP start/stop
+events on every launch of a second timed pass over further sweeps of the same run (per-launch
+events force host-issued launches, so that pass gives kernel durations, not `value`); traffic
+from the committed rocprofv3 PMC summary.  cpu_baseline: the bitwise-pinned numpy restatement of
+the reference (oracle/ref_cpu.py) on 1 core.
 """
 from __future__ import annotations
 
@@ -43,6 +46,26 @@ def algorithmic_bytes(D: int, K: int, thin: int, draw_sink: str) -> float:
     wr = 16
     draws = 8.0 * (D + 2) / thin if draw_sink == "full" else (8.0 * 2 * (7 if D == 2 else 9) / thin if draw_sink == "summary" else 0.0)
     return rd + wr + draws
+
+
+def committed_traffic(workload: str, world: int):
+    """HBM bytes per sweep-kernel launch from the committed rocprofv3 PMC summary of this workload
+    (profiles/*_summary.json written by tools/summarize_profile.py): FETCH_SIZE + WRITE_SIZE,
+    uncorrected (see DESIGN.md §Roofline for the gfx950 FETCH_SIZE caveat); None if absent."""
+    import glob
+    if world != 1:
+        return None
+    best = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{workload}_*summary.json"))):
+        try:
+            d = json.load(open(path))
+        except Exception:
+            continue
+        for name, k in d.get("kernels", {}).items():
+            if "sweep_kernel" in name and "traffic_bytes_uncorrected" in k:
+                best = dict(bytes_per_launch=round(k["traffic_bytes_uncorrected"]), source=os.path.basename(path),
+                            counters="FETCH_SIZE+WRITE_SIZE (x1024, uncorrected)")
+    return best
 
 
 def load_workload(name: str):
@@ -104,8 +127,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1000)
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-kernel-timing", action="store_true",
-                    help="replay captured hipGraphs in the timed region instead of event-timed launches")
+    ap.add_argument("--no-kernel-timing", action="store_true", help="skip the event-timed roofline pass")
+    ap.add_argument("--timing-steps", type=int, default=3000, help="sweeps in the event-timed roofline pass")
     ap.add_argument("--cpu-baseline-child", action="store_true")
     ap.add_argument("--cpu-warm", type=int, default=20)
     ap.add_argument("--cpu-timed", type=int, default=200)
@@ -132,7 +155,7 @@ def main():
     from mcmc_clv_model_amd.sampler import HipSampler, build_problem
 
     df, D, covs, chains, burnin, mcmc, thin, sink = load_workload(a.workload)
-    total = a.warmup + a.steps
+    total = a.warmup + a.steps + (0 if a.no_kernel_timing else min(a.steps, a.timing_steps))
     mcmc = max(mcmc, total - burnin)
     n_per_rank = len(df)
     if world == 1:
@@ -154,16 +177,14 @@ def main():
         kern = ss.s
 
     K = len(covs) + 1
-    timing = not a.no_kernel_timing and world == 1
+    timing = not a.no_kernel_timing
     run(a.warmup)
     sync()
-    if timing:
-        kern.set_timing(True)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    run(a.steps)
+    run(a.steps)                      # timed region: hipGraph replay (world 1) / sharded steps
     sync()
     torch.cuda.synchronize()
     if dist:
@@ -176,19 +197,28 @@ def main():
     units = chains * n_per_rank * world * a.steps
     value = units / dt
 
+    # Roofline pass: the same sweeps continue, each sweep launch carrying HIP start/stop events
+    # (hipExtLaunchKernelGGL: the dispatch's own timestamps).  Launches are then host-issued,
+    # which leaves gaps between kernels, so this pass yields kernel durations, not `value`.
     roofline = None
-    kt = kern.kernel_time() if timing else None
     bpu = algorithmic_bytes(D, K, thin, sink)
-    if kt and kt["sweep_launches"]:
-        t_launch = kt["sweep_ms"] / kt["sweep_launches"] * 1e-3
-        achieved = bpu * chains * n_per_rank / t_launch / 1e9
-        roofline = dict(bound="hbm", achieved=round(achieved, 3), peak=HBM_PEAK_GBS, unit="GB/s",
-                        frac=round(achieved / HBM_PEAK_GBS, 6), traffic=None,
-                        kernel="sweep_kernel", bytes_per_unit=bpu,
-                        units_per_launch=chains * n_per_rank,
-                        sweep_kernel_us=round(t_launch * 1e6, 3),
-                        hyper_kernel_us=round(kt["hyper_ms"] / max(kt["hyper_launches"], 1) * 1e3, 3),
-                        launches=kt["sweep_launches"])
+    if timing:
+        kern.set_timing(True)
+        n_t = min(a.steps, a.timing_steps)
+        run(n_t)
+        sync()
+        kt = kern.kernel_time()
+        kern.set_timing(False)
+        if kt["sweep_launches"]:
+            t_launch = kt["sweep_ms"] / kt["sweep_launches"] * 1e-3
+            achieved = bpu * chains * n_per_rank / t_launch / 1e9
+            roofline = dict(bound="hbm", achieved=round(achieved, 3), peak=HBM_PEAK_GBS, unit="GB/s",
+                            frac=round(achieved / HBM_PEAK_GBS, 6), traffic=committed_traffic(a.workload, world),
+                            kernel="sweep_kernel (incl. fused level-2 tail)" if world == 1 else "sweep_kernel",
+                            bytes_per_unit=bpu, units_per_launch=chains * n_per_rank,
+                            sweep_kernel_us=round(t_launch * 1e6, 3), timed_launches=kt["sweep_launches"])
+            if kt["hyper_launches"]:
+                roofline["hyper_kernel_us"] = round(kt["hyper_ms"] / kt["hyper_launches"] * 1e3, 3)
 
     if rank == 0:
         cpu = None
@@ -204,7 +234,8 @@ def main():
             config=dict(workload=f"{a.workload}: {'bivariate' if D == 2 else 'trivariate'} M2, covariates {covs}",
                         n_customers=n_per_rank * world, chains=chains, n_mh_steps=20, burnin=burnin, mcmc=mcmc,
                         thin=thin, seed=42, draw_sink=sink, parallelism=f"customer-shard x{world}",
-                        timed_region="event-timed launches" if timing else "hipGraph replay"),
+                        timed_region="hipGraph replay of fused sweep launches" if world == 1 else
+                        "sweep + RCCL all_gather + level-2 launches per step"),
             roofline=roofline, cpu_baseline=cpu,
             speedup_vs_cpu_1core=(value / cpu["value"]) if cpu else None,
         )

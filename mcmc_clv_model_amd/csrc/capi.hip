@@ -59,6 +59,7 @@ struct clv_sampler {
   double* d_prior = nullptr;
   Ctrl* d_ctrl = nullptr;
   uint32_t* d_arrive = nullptr;     // [chain] fused-tail arrival counters
+  double* d_hvar = nullptr;         // [chain][HV] precomputed hyper variates
   double *d_level1 = nullptr, *d_level2 = nullptr, *d_loglik = nullptr, *d_sums = nullptr;
   double* d_tape = nullptr;
   double* d_bs = nullptr;  // staging for set_hyper
@@ -106,7 +107,9 @@ SweepArgs sweep_args(clv_sampler* s, int init, int fuse = 0) {
   a.init = init;
   a.fuse = fuse;
   a.chain_arrive = s->d_arrive;
-  if (fuse) a.h = hyper_args(s, nullptr, 0);
+  a.hvar_out = s->d_hvar;
+  a.h = hyper_args(s, nullptr, 0);
+  if (fuse) a.h.hvar = s->replay ? nullptr : s->d_hvar;
   return a;
 }
 
@@ -130,13 +133,13 @@ HyperArgs hyper_args(clv_sampler* s, const double* units, int mode) {
   a.nu_n = s->prior.nu_n;
   a.omega2 = s->prior.omega2;
   a.mode = mode;
+  // mode 0 follows a sweep kernel, which precomputed the draw's variates (if it had workgroups)
+  a.hvar = (mode == 0 && !s->replay && s->g.nb_local > 0) ? s->d_hvar : nullptr;
   return a;
 }
 
 int enqueue_sweep(clv_sampler* s, hipEvent_t e0, hipEvent_t e1) {
-  if (e0) CLV_HIP(hipEventRecord(e0, s->stream));
-  CLV_HIP(launch_sweep(sweep_args(s, 0), s->replay, s->stream));
-  if (e1) CLV_HIP(hipEventRecord(e1, s->stream));
+  CLV_HIP(launch_sweep(sweep_args(s, 0), s->replay, s->stream, e0, e1));
   if (s->g.blocks_per_unit > 1) {
     GroupArgs ga{};
     ga.g = s->g;
@@ -149,9 +152,7 @@ int enqueue_sweep(clv_sampler* s, hipEvent_t e0, hipEvent_t e1) {
 
 // world_size == 1: one launch per sweep (the level-2 draw runs in the sweep kernel's tail)
 int enqueue_fused(clv_sampler* s, hipEvent_t e0, hipEvent_t e1) {
-  if (e0) CLV_HIP(hipEventRecord(e0, s->stream));
-  CLV_HIP(launch_sweep(sweep_args(s, 0, 1), s->replay, s->stream));
-  if (e1) CLV_HIP(hipEventRecord(e1, s->stream));
+  CLV_HIP(launch_sweep(sweep_args(s, 0, 1), s->replay, s->stream, e0, e1));
   return CLV_OK;
 }
 
@@ -182,6 +183,14 @@ int harvest_timing(clv_sampler* s) {
     (void)0;  // fused: the level-2 draw is inside the timed sweep launch
   }
   s->ev_used = 0;
+  return CLV_OK;
+}
+
+int ensure_events(clv_sampler* s) {
+  if (s->ev.empty()) {
+    s->ev.resize(4 * TIMING_EVENTS);
+    for (auto& e : s->ev) CLV_HIP(hipEventCreate(&e));
+  }
   return CLV_OK;
 }
 
@@ -345,6 +354,8 @@ int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* pri
   CLV_HIPC(dalloc(&s->d_prior, PRIOR_DOUBLES));
   CLV_HIPC(dalloc(&s->d_ctrl, 1));
   CLV_HIPC(dalloc(&s->d_arrive, C));
+  CLV_HIPC(dalloc(&s->d_hvar, C * HV));
+  CLV_HIPC(hipMemsetAsync(s->d_hvar, 0, sizeof(double) * C * HV, s->stream));
   CLV_HIPC(hipMemsetAsync(s->d_arrive, 0, sizeof(uint32_t) * C, s->stream));
   CLV_HIPC(dalloc(&s->d_bs, C * (CLV_MAX_K * CLV_MAX_D + CLV_MAX_D * CLV_MAX_D)));
   if (g.n_draws > 0) {
@@ -425,7 +436,7 @@ void clv_destroy(clv_sampler* s) {
   for (auto e : s->ev) (void)hipEventDestroy(e);
   void* ptrs[] = {s->d_x, s->d_tx, s->d_T, s->d_cov, s->d_logs, s->d_lam, s->d_mu, s->d_hyper,
                   s->d_block, s->d_prior, s->d_ctrl, s->d_level1, s->d_level2, s->d_loglik,
-                  s->d_sums, s->d_tape, s->d_bs, s->d_arrive};
+                  s->d_sums, s->d_tape, s->d_bs, s->d_arrive, s->d_hvar};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (s->d_unit && s->d_unit != s->d_block) (void)hipFree(s->d_unit);
@@ -471,8 +482,19 @@ int clv_sweep(clv_sampler* s) {
   CLV_HIP(hipSetDevice(s->device));
   int rc = check_replay_range(s, 1);
   if (rc) return rc;
-  rc = enqueue_sweep(s, nullptr, nullptr);
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (s->timing) {
+    rc = ensure_events(s);
+    if (rc) return rc;
+    e0 = s->ev[4 * s->ev_used];
+    e1 = s->ev[4 * s->ev_used + 1];
+  }
+  rc = enqueue_sweep(s, e0, e1);
   if (rc) return rc;
+  if (s->timing && ++s->ev_used == TIMING_EVENTS) {
+    rc = harvest_timing(s);
+    if (rc) return rc;
+  }
   s->sweeps_done++;
   return CLV_OK;
 }
@@ -516,10 +538,8 @@ int clv_run(clv_sampler* s, int64_t n_sweeps) {
   }
   int64_t left = n_sweeps;
   if (s->timing) {
-    if (s->ev.empty()) {
-      s->ev.resize(4 * TIMING_EVENTS);
-      for (auto& e : s->ev) CLV_HIP(hipEventCreate(&e));
-    }
+    rc = ensure_events(s);
+    if (rc) return rc;
     while (left > 0) {
       const int k = s->ev_used;
       rc = enqueue_fused(s, s->ev[4 * k], s->ev[4 * k + 1]);
@@ -631,6 +651,8 @@ int clv_set_state(clv_sampler* s, const double* lambdas, const double* mus, cons
 
 int clv_set_timing(clv_sampler* s, int32_t enable) {
   if (!s) return fail(CLV_EINVAL, "null sampler");
+  int rc = harvest_timing(s);  // never drop pending timed launches
+  if (rc) return rc;
   s->timing = enable != 0;
   s->t_sweep_ms = s->t_hyper_ms = 0.0;
   s->n_sweep_timed = s->n_hyper_timed = 0;
@@ -639,6 +661,8 @@ int clv_set_timing(clv_sampler* s, int32_t enable) {
 
 int clv_kernel_time(clv_sampler* s, double* sweep_ms, int64_t* n_sweep, double* hyper_ms, int64_t* n_hyper) {
   if (!s) return fail(CLV_EINVAL, "null sampler");
+  int rc = harvest_timing(s);
+  if (rc) return rc;
   if (sweep_ms) *sweep_ms = s->t_sweep_ms;
   if (n_sweep) *n_sweep = s->n_sweep_timed;
   if (hyper_ms) *hyper_ms = s->t_hyper_ms;

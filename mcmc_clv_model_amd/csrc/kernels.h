@@ -10,6 +10,8 @@ namespace clv {
 constexpr int BLOCK = CLV_BLOCK;       // customers (lanes) per sweep workgroup
 constexpr int HS = 64;                 // doubles of hyper state per chain
 constexpr int TAPE_HYPER = 40;         // doubles of hyper variates per recorded sweep
+constexpr int HV = 40;                 // precomputed Philox hyper variates per chain: iw normals [0,3),
+                                       // chi2 [3,6), beta normals [8,35)
 
 // Hyper-state layout (per chain, HS doubles).
 enum : int {
@@ -66,6 +68,7 @@ struct HyperArgs {
   double nu_n;
   double omega2;
   int mode;                  // 0: after sweep (cur+1); 1: bivariate initial draw (sweep 1)
+  const double* hvar;        // [chain][HV] Philox variates precomputed by the sweep kernel, or null
 };
 
 struct SweepArgs {
@@ -88,6 +91,8 @@ struct SweepArgs {
   int init;                  // 1: initialisation pass (bi:367-370), no sweep
   int fuse;                  // 1: the chain's last-arriving workgroup performs the level-2 draw
   uint32_t* chain_arrive;    // [chain] arrival counters of the fused tail (zero between launches)
+  double* hvar_out;          // [chain][HV]: the chain's last workgroup precomputes the next level-2
+                             // draw's Philox variates at its start (off the critical path), or null
   HyperArgs h;               // level-2 arguments of the fused tail
 };
 
@@ -99,7 +104,8 @@ struct GroupArgs {
 
 
 // Launchers (kernels.hip).
-hipError_t launch_sweep(const SweepArgs& a, bool replay, hipStream_t st);
+hipError_t launch_sweep(const SweepArgs& a, bool replay, hipStream_t st, hipEvent_t e0 = nullptr,
+                        hipEvent_t e1 = nullptr);
 hipError_t launch_group(const GroupArgs& a, hipStream_t st);
 hipError_t launch_hyper(const HyperArgs& a, bool replay, hipStream_t st);
 hipError_t launch_set_hyper(int D, int K, int n_chains, double* hyper, const double* beta_sigma,

@@ -11,10 +11,14 @@
 // Reference: src/models/bivariate/mcmc.py (bi), src/models/trivariate/mcmc.py (tri).
 // All model arithmetic is float64 and follows the reference's operation order, so that with
 // replayed variates (CLV_RNG_REPLAY) trajectories agree with the reference to rounding.
+#include <hip/hip_ext.h>
+
 #include "kernels.h"
 #include "philox.h"
 
 namespace clv {
+
+constexpr int MH_CHUNK = 4;  // MH steps whose variates are generated one chunk ahead
 
 __device__ __forceinline__ double clip70(double v) {  // np.clip(v, -70, 70), NaN passes (bi:323)
   return v < -70.0 ? -70.0 : (v > 70.0 ? 70.0 : v);
@@ -297,7 +301,8 @@ __device__ void hyper_body(const HyperArgs& a, int c, int64_t s, int mode, const
 #pragma unroll
       for (int j = 0; j < NS; ++j) {
         double t = 0.0;
-        for (int bb = 0; bb < g.blocks_per_unit; ++bb) t += p[(int64_t)bb * g.stride + j];
+        for (int bb = 0; bb < g.blocks_per_unit; ++bb)
+          t += __hip_atomic_load(p + (int64_t)bb * g.stride + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         acc[j] += t;
       }
     } else {
@@ -317,6 +322,11 @@ __device__ void hyper_body(const HyperArgs& a, int c, int64_t s, int mode, const
     if (tid < 3) var_iw[tid] = tv[tid];
     if (tid < 3) var_chi[tid] = tv[3 + tid];
     if (tid < D * K) var_noise[tid] = tv[6 + tid];
+  } else if (a.hvar) {  // precomputed by this sweep's kernel (sc1 stores: read with sc1 loads)
+    const double* hv = a.hvar + (int64_t)c * HV;
+    if (tid < 3) var_iw[tid] = __hip_atomic_load(hv + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid < 3) var_chi[tid] = __hip_atomic_load(hv + 3 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid < D * K) var_noise[tid] = __hip_atomic_load(hv + 8 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   } else {
     uint32_t k0, k1;
     chain_key(a.r.seed, (int64_t)a.r.chain_first + c, &k0, &k1);
@@ -394,6 +404,31 @@ __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
   double acc[NS];
 #pragma unroll
   for (int j = 0; j < NS; ++j) acc[j] = 0.0;
+
+  // ---- the next level-2 draw's Philox variates (independent of the statistics): computed by
+  // wave 3 of the chain's last workgroup — the partially filled one — so the draw's serial
+  // tail only loads them.  Written with sc1 (write-through) stores.
+  if constexpr (!REPLAY) {
+    if (a.hvar_out && !a.init && b == g.nb_local - 1 && (threadIdx.x >> 6) == 3) {
+      const int l = threadIdx.x & 63;
+      const int64_t hs = (D == 2) ? s + 1 : s;
+      uint32_t k0, k1;
+      chain_key(a.r.seed, (int64_t)a.r.chain_first + c, &k0, &k1);
+      double v = 0.0;
+      int slot = -1;
+      if (l < D * (D - 1) / 2) {
+        v = hyper_normal(k0, k1, HSLOT_NORMAL0 + l, (uint32_t)hs);
+        slot = l;
+      } else if (l >= 8 && l < 8 + D * K) {
+        v = hyper_normal(k0, k1, HSLOT_BETA_NORMAL0 + (l - 8), (uint32_t)hs);
+        slot = l;
+      } else if (l >= 40 && l < 40 + D) {
+        v = chi2_draw(k0, k1, (uint32_t)hs, l - 40, a.h.nu_n - D + 1 + (l - 40));
+        slot = 3 + (l - 40);
+      }
+      if (slot >= 0) __hip_atomic_store(a.hvar_out + (int64_t)c * HV + slot, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 
   if (active) {
     const double* H = a.hyper + (int64_t)c * HS;
@@ -483,31 +518,65 @@ __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
       double ll = log(lam);
       double lm = log(mu);
       double cur = log_post(lc, ll, lm);
-      for (int j = 0; j < g.S; ++j) {
-        double pl, pm, plp;
-        bool accept;
-        if constexpr (REPLAY) {
+      if constexpr (REPLAY) {
+        for (int j = 0; j < g.S; ++j) {
           const double tl = tape[(int64_t)(2 + 3 * j) * g.n + i];
           const double tm = tape[(int64_t)(3 + 3 * j) * g.n + i];
           const double u = tape[(int64_t)(4 + 3 * j) * g.n + i];
-          pl = clip70(ll + s00 * tl);
-          pm = clip70(lm + s11 * tm);
-          plp = log_post(lc, pl, pm);
-          accept = exp(plp - cur) > u;           // bi:329-330
-        } else {
+          const double pl = clip70(ll + s00 * tl);
+          const double pm = clip70(lm + s11 * tm);
+          const double plp = log_post(lc, pl, pm);
+          if (exp(plp - cur) > u) {  // bi:329-335
+            ll = pl;
+            lm = pm;
+            cur = plp;
+          }
+        }
+      } else {
+        // Software pipeline: the Philox blocks and t3 transforms of the next MH_CHUNK steps are
+        // independent of the state, so they are generated while the current chunk's fp64
+        // accept/reject chain runs (ILP for the ~1.5 waves/SIMD of the CDNOW-sized problem).
+        constexpr int MC = MH_CHUNK;
+        float tl[MC], tm[MC], lu[MC];
+        auto gen = [&](int j0, float (&a)[MC], float (&b)[MC], float (&c)[MC]) {
+#pragma unroll
+          for (int q = 0; q < MC; ++q) {
+            const uint32_t j = (uint32_t)(j0 + q);
+            const u32x4 ra = customer_block(k0, k1, gi, (uint32_t)s, SLOT_MH0 + 2u * j);
+            const u32x4 rb = customer_block(k0, k1, gi, (uint32_t)s, SLOT_MH0 + 2u * j + 1u);
+            mh_variates(ra, rb, &a[q], &b[q], &c[q]);
+          }
+        };
+        auto step = [&](float t_l, float t_m, float l_u) {
+          const double pl = clip70(ll + s00 * (double)t_l);
+          const double pm = clip70(lm + s11 * (double)t_m);
+          const double plp = log_post(lc, pl, pm);
+          if ((plp - cur) > (double)l_u) {  // exp(d) > u  <=>  d > log(u)
+            ll = pl;
+            lm = pm;
+            cur = plp;
+          }
+        };
+        const int S_full = g.S - g.S % MC;
+        if (S_full > 0) gen(0, tl, tm, lu);
+        for (int j0 = 0; j0 < S_full; j0 += MC) {
+          float ntl[MC], ntm[MC], nlu[MC];
+          if (j0 + MC < S_full) gen(j0 + MC, ntl, ntm, nlu);
+#pragma unroll
+          for (int q = 0; q < MC; ++q) step(tl[q], tm[q], lu[q]);
+#pragma unroll
+          for (int q = 0; q < MC; ++q) {
+            tl[q] = ntl[q];
+            tm[q] = ntm[q];
+            lu[q] = nlu[q];
+          }
+        }
+        for (int j = S_full; j < g.S; ++j) {  // remainder steps
           const u32x4 ra = customer_block(k0, k1, gi, (uint32_t)s, SLOT_MH0 + 2u * j);
           const u32x4 rb = customer_block(k0, k1, gi, (uint32_t)s, SLOT_MH0 + 2u * j + 1u);
-          float tl, tm, lu;
-          mh_variates(ra, rb, &tl, &tm, &lu);
-          pl = clip70(ll + s00 * (double)tl);
-          pm = clip70(lm + s11 * (double)tm);
-          plp = log_post(lc, pl, pm);
-          accept = (plp - cur) > (double)lu;     // exp(d) > u  <=>  d > log(u)
-        }
-        if (accept) {
-          ll = pl;
-          lm = pm;
-          cur = plp;
+          float a1, b1, c1;
+          mh_variates(ra, rb, &a1, &b1, &c1);
+          step(a1, b1, c1);
         }
       }
       lam = exp(ll);  // bi:337-338
@@ -586,31 +655,28 @@ __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
   }
 
   block_reduce<NS>(acc, red, tot);
-  if (threadIdx.x < NS)
-    a.blockpart[((int64_t)c * g.blocks_per_rank + b) * g.stride + threadIdx.x] = tot[threadIdx.x];
+  if (threadIdx.x < NS)  // sc1 (write-through) store: read cross-CU by the fused tail
+    __hip_atomic_store(a.blockpart + ((int64_t)c * g.blocks_per_rank + b) * g.stride + threadIdx.x, tot[threadIdx.x],
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
   // ---- fused level-2 draw (world_size == 1): the chain's last workgroup to arrive reduces all
-  // block partials and draws (beta, Sigma) — no separate hyper launch per sweep.  Hand-off per
-  // MI355X guide Guideline 16: stores drained, agent release, atomic ticket; the last arriver
-  // takes an agent acquire before reading the other workgroups' partials.
+  // block partials and draws (beta, Sigma) — no separate hyper launch per sweep.  Hand-off in the
+  // fence-free form of the MI355X guide (Guideline 16 / "Valid forms"): partials and variates are
+  // stored sc1 (write-through), every wave drains its stores, one lane takes an agent-scope
+  // ticket; the last arriver reads every handed-off value with sc1 loads (no L1 hit possible).
   if (a.fuse) {
     __shared__ uint32_t s_last;
     __shared__ double var_iw[4], var_chi[4], var_noise[32];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const uint32_t old = __hip_atomic_fetch_add(a.chain_arrive + c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const uint32_t last = old == (uint32_t)(g.nb_local - 1) ? 1u : 0u;
-      if (last) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(a.chain_arrive + c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+      if (last) __hip_atomic_store(a.chain_arrive + c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       s_last = last;
     }
     __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only
     if (s_last) hyper_body<D, K, REPLAY, NS>(a.h, c, s, 0, a.blockpart, red, tot, var_iw, var_chi, var_noise);
   }
 }
@@ -706,11 +772,17 @@ __global__ void debug_hyper_variates_kernel(uint64_t seed, int chain, uint32_t s
 #define CLV_FOR_K(M, D, R) \
   M(D, 1, R) M(D, 2, R) M(D, 3, R) M(D, 4, R) M(D, 5, R) M(D, 6, R) M(D, 7, R) M(D, 8, R) M(D, 9, R)
 
-hipError_t launch_sweep(const SweepArgs& a, bool replay, hipStream_t st) {
+hipError_t launch_sweep(const SweepArgs& a, bool replay, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
   const dim3 grid(a.g.nb_local, a.g.n_chains);
   const dim3 block(BLOCK);
-#define CLV_CASE(DD, KK, RR) \
-  if (a.g.D == DD && a.g.K == KK && replay == RR) { hipLaunchKernelGGL((sweep_kernel<DD, KK, RR>), grid, block, 0, st, a); return hipGetLastError(); }
+  // e0/e1: hipExtLaunchKernelGGL records the dispatch's own start/end timestamps into the events
+  // (no extra marker packets in the stream, unlike hipEventRecord around the launch).
+#define CLV_CASE(DD, KK, RR)                                                                      \
+  if (a.g.D == DD && a.g.K == KK && replay == RR) {                                               \
+    if (e0) hipExtLaunchKernelGGL((sweep_kernel<DD, KK, RR>), grid, block, 0, st, e0, e1, 0, a); \
+    else hipLaunchKernelGGL((sweep_kernel<DD, KK, RR>), grid, block, 0, st, a);                   \
+    return hipGetLastError();                                                                     \
+  }
   CLV_FOR_K(CLV_CASE, 2, false)
   CLV_FOR_K(CLV_CASE, 3, false)
   CLV_FOR_K(CLV_CASE, 2, true)

@@ -1,0 +1,79 @@
+#!/usr/bin/env python
+"""Summarise a tools/gpu_profile.sh run (gpurun_out/prof/*) into profiles/<tag>_summary.json and
+copy the rocprofv3 --stats table next to it.
+
+Per kernel: average duration (kernel-trace), FETCH_SIZE / WRITE_SIZE per dispatch (KB as reported
+by rocprofv3; gfx950 note in DESIGN.md: FETCH_SIZE under-counts wide streaming reads by 2x and is
+uncalibrated for 4/8-B-per-lane loads), VALU instructions and active cycles per wave, waves, and
+the effective clock from GRBM_GUI_ACTIVE.
+"""
+import csv
+import json
+import os
+import shutil
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def mean_counter(path, counter):
+    out = {}
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != counter:
+            continue
+        out.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
+    return {k: statistics.mean(v) for k, v in out.items()}
+
+
+def main(tag, prof=os.path.join(ROOT, "gpurun_out", "prof"), bench_log=None):
+    os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
+    stats = list(csv.DictReader(open(os.path.join(prof, "trace", "run_kernel_stats.csv"))))
+    shutil.copy(os.path.join(prof, "trace", "run_kernel_stats.csv"), os.path.join(ROOT, "profiles", f"{tag}_kernel_stats.csv"))
+    trace = list(csv.DictReader(open(os.path.join(prof, "trace", "run_kernel_trace.csv"))))
+    res = {"tag": tag, "kernels": {}}
+    fetch = mean_counter(os.path.join(prof, "fetch_size", "run_counter_collection.csv"), "FETCH_SIZE")
+    write = mean_counter(os.path.join(prof, "write_size", "run_counter_collection.csv"), "WRITE_SIZE")
+    vpath = os.path.join(prof, "sq_insts_valu", "run_counter_collection.csv")
+    valu = {c: mean_counter(vpath, c) for c in ("SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "SQ_WAVE_CYCLES", "SQ_WAVES",
+                                               "SQ_BUSY_CYCLES", "GRBM_GUI_ACTIVE")}
+    for r in stats:
+        name = r["Name"]
+        if name.startswith("__amd"):
+            continue
+        k = dict(calls=int(r["Calls"]), avg_ns=float(r["AverageNs"]), min_ns=float(r["MinNs"]), max_ns=float(r["MaxNs"]),
+                 stddev_ns=float(r["StdDev"]))
+        rows = [t for t in trace if t["Kernel_Name"] == name]
+        if len(rows) > 2:
+            st = [int(t["Start_Timestamp"]) for t in rows]
+            en = [int(t["End_Timestamp"]) for t in rows]
+            k["median_gap_ns"] = statistics.median([st[i + 1] - en[i] for i in range(len(rows) - 1)])
+        if name in fetch:
+            k["fetch_size_kb"] = fetch[name]
+        if name in write:
+            k["write_size_kb"] = write[name]
+        if name in fetch and name in write:
+            k["traffic_bytes_uncorrected"] = (fetch[name] + write[name]) * 1024
+        if name in valu["SQ_WAVES"]:
+            waves = valu["SQ_WAVES"][name]
+            k["waves"] = waves
+            k["valu_insts_per_wave"] = valu["SQ_INSTS_VALU"][name] / waves
+            k["valu_active_quadcycles_per_wave"] = valu["SQ_ACTIVE_INST_VALU"][name] / waves
+            k["wave_quadcycles_per_wave"] = valu["SQ_WAVE_CYCLES"][name] / waves
+            k["valu_active_frac_of_wave_lifetime"] = valu["SQ_ACTIVE_INST_VALU"][name] / valu["SQ_WAVE_CYCLES"][name]
+            gui = valu["GRBM_GUI_ACTIVE"][name]
+            k["grbm_gui_active"] = gui
+        res["kernels"][name] = k
+    if bench_log and os.path.exists(bench_log):
+        for line in open(bench_log):
+            if line.startswith("{"):
+                res["bench_line_under_profiler"] = json.loads(line)
+    out = os.path.join(ROOT, "profiles", f"{tag}_summary.json")
+    json.dump(res, open(out, "w"), indent=1)
+    print(out)
+    for n, k in res["kernels"].items():
+        print(n[:70], {a: (round(b, 3) if isinstance(b, float) else b) for a, b in k.items()})
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], bench_log=os.path.join(ROOT, "gpurun_out", "prof_trace.log"))
