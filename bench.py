@@ -31,29 +31,33 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 
 WORKLOADS = {
-    # name: (D, data, covariates, chains, burnin, mcmc, thin, draw_sink)
-    "c2": (2, "full", ["first_sales_scaled"], 4, 10000, 10000, 10, "full"),
+    # name: (D, data, covariates, chains, burnin, mcmc, thin, draw_sink)   (SURVEY.md §8 notation)
+    "c1": (2, "abe", [], 4, 10000, 4000, 1, "full"),                      # run_mcmc_abe.py:61-71
+    "c2": (2, "full", ["first_sales_scaled"], 4, 10000, 10000, 10, "full"),  # BASELINE configs[1]
     "c3": (3, "full", ["gender_F", "age_scaled"], 4, 10000, 10000, 10, "full"),
-    "c1": (2, "abe", [], 4, 10000, 4000, 1, "full"),
+    # synthetic: 1M customers K=5 bivariate; 1.25M customers per GPU K=9 trivariate
+    "c4": (2, "synthetic:1000000:5:20250718", ["c1", "c2", "c3", "c4"], 1, 5000, 5000, 1, "summary"),
+    "c5": (3, "synthetic:1250000:9:20250719", [f"c{k}" for k in range(1, 9)], 1, 5000, 5000, 1, "summary"),
 }
 
 
-def algorithmic_bytes(D: int, K: int, thin: int, draw_sink: str) -> float:
-    """HBM bytes one (chain, customer) moves per sweep in the sweep kernel (DESIGN.md §Roofline):
+def algorithmic_bytes(D: int, K: int, stored_frac: float, draw_sink: str) -> float:
+    """HBM bytes one (chain, customer) moves per sweep in the sweep kernel (DESIGN.md §4):
     read x (4) + t_x, T (16) + K-1 covariates (8 each) + log_s (D=3: 8) + lambda, mu (16);
-    write lambda, mu (16); level-1 draw (8(D+2)) amortised over thin when stored."""
+    write lambda, mu (16); per stored sweep (share `stored_frac`): the level-1 draw 8(D+2)
+    (full sink) or the read-modify-write of 7 (D=2) / 9 (D=3) running sums (summary sink)."""
     rd = 4 + 16 + 8 * (K - 1) + (8 if D == 3 else 0) + 16
     wr = 16
-    draws = 8.0 * (D + 2) / thin if draw_sink == "full" else (8.0 * 2 * (7 if D == 2 else 9) / thin if draw_sink == "summary" else 0.0)
-    return rd + wr + draws
+    per_store = 8.0 * (D + 2) if draw_sink == "full" else (16.0 * (7 if D == 2 else 9) if draw_sink == "summary" else 0.0)
+    return rd + wr + per_store * stored_frac
 
 
-def committed_traffic(workload: str, world: int):
+def committed_traffic(workload: str, sharded: bool):
     """HBM bytes per sweep-kernel launch from the committed rocprofv3 PMC summary of this workload
     (profiles/*_summary.json written by tools/summarize_profile.py): FETCH_SIZE + WRITE_SIZE,
     uncorrected (see DESIGN.md §Roofline for the gfx950 FETCH_SIZE caveat); None if absent."""
     import glob
-    if world != 1:
+    if sharded:
         return None
     best = None
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{workload}_*summary.json"))):
@@ -68,14 +72,29 @@ def committed_traffic(workload: str, world: int):
     return best
 
 
-def load_workload(name: str):
+def load_workload(name: str, world: int = 1):
+    """CBS of a workload.  CDNOW: the committed CBS columns (weak scaling: one copy per rank).
+    Synthetic: mcmc_clv_model_amd.data.synthetic_cbs with n per GPU (c5 weak scaling: n x world)."""
     import numpy as np
     import pandas as pd
-    from mcmc_clv_model_amd.data import add_driver_columns
+    from mcmc_clv_model_amd.data import add_driver_columns, synthetic_cbs
     D, data, covs, chains, burnin, mcmc, thin, sink = WORKLOADS[name]
-    d = np.load(os.path.join(ROOT, "tests", "golden", f"cdnow_{data}_cbs.npz"), allow_pickle=False)
-    df = add_driver_columns(pd.DataFrame({k: d[k] for k in d.files}))
+    if data.startswith("synthetic:"):
+        _, n, K, seed = data.split(":")
+        n = int(n) * (world if name == "c5" else 1)
+        df = synthetic_cbs(n, int(K), D, seed=int(seed))
+    else:
+        d = np.load(os.path.join(ROOT, "tests", "golden", f"cdnow_{data}_cbs.npz"), allow_pickle=False)
+        df = add_driver_columns(pd.DataFrame({k: d[k] for k in d.files}))
+        if world > 1:
+            df = pd.concat([df] * world, ignore_index=True)
     return df, D, covs, chains, burnin, mcmc, thin, sink
+
+
+def stored_fraction(burnin: int, thin: int, first: int, last: int) -> float:
+    """Share of sweeps first..last (1-based, inclusive) that store a draw (bi:402)."""
+    n = sum(1 for s in range(first, last + 1) if s > burnin and (s - 1 - burnin) % thin == 0)
+    return n / max(1, last - first + 1)
 
 
 def cpu_baseline_child(workload: str, warm: int, timed: int) -> None:
@@ -107,6 +126,8 @@ def cpu_baseline_child(workload: str, warm: int, timed: int) -> None:
 
 
 def cpu_baseline(workload: str, warm: int = 20, timed: int = 200):
+    if WORKLOADS[workload][1].startswith("synthetic:"):  # ~3 s/sweep on one core
+        warm, timed = 2, 5
     env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1",
                HIP_VISIBLE_DEVICES="", ROCR_VISIBLE_DEVICES="")
     out = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-baseline-child", "--workload", workload,
@@ -129,6 +150,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true", help="skip the event-timed roofline pass")
     ap.add_argument("--timing-steps", type=int, default=3000, help="sweeps in the event-timed roofline pass")
+    ap.add_argument("--force-sharded", action="store_true",
+                    help="use the sharded path (torch.distributed exchange) even at world size 1")
     ap.add_argument("--cpu-baseline-child", action="store_true")
     ap.add_argument("--cpu-warm", type=int, default=20)
     ap.add_argument("--cpu-timed", type=int, default=200)
@@ -146,19 +169,24 @@ def main():
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
     dist = None
-    if world > 1:
+    sharded = world > 1 or a.force_sharded
+    if sharded:
         import torch.distributed as dist
         torch.cuda.set_device(local_rank)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
 
     from mcmc_clv_model_amd import _lib
     from mcmc_clv_model_amd.sampler import HipSampler, build_problem
 
-    df, D, covs, chains, burnin, mcmc, thin, sink = load_workload(a.workload)
+    df, D, covs, chains, burnin, mcmc, thin, sink = load_workload(a.workload, world)
     total = a.warmup + a.steps + (0 if a.no_kernel_timing else min(a.steps, a.timing_steps))
     mcmc = max(mcmc, total - burnin)
-    n_per_rank = len(df)
-    if world == 1:
+    n_total = len(df)
+    if not sharded:
         p = build_problem(df, covs, D)
         s = HipSampler(p, mcmc=mcmc, burnin=burnin, thin=thin, chains=chains, seed=42, draw_sink=sink,
                        device=local_rank)
@@ -166,10 +194,8 @@ def main():
         sync = s.synchronize
         kern = s
     else:
-        import pandas as pd
         from mcmc_clv_model_amd.distributed import ShardedSampler
-        tiled = pd.concat([df] * world, ignore_index=True)
-        p = build_problem(tiled, covs, D)
+        p = build_problem(df, covs, D)
         ss = ShardedSampler(p, rank=rank, world=world, chains=chains, mcmc=mcmc, burnin=burnin, thin=thin, seed=42,
                             draw_sink=sink, device=local_rank)
         run = ss.step
@@ -194,14 +220,16 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local_rank}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    units = chains * n_per_rank * world * a.steps
+    units = chains * n_total * a.steps
     value = units / dt
 
     # Roofline pass: the same sweeps continue, each sweep launch carrying HIP start/stop events
     # (hipExtLaunchKernelGGL: the dispatch's own timestamps).  Launches are then host-issued,
     # which leaves gaps between kernels, so this pass yields kernel durations, not `value`.
     roofline = None
-    bpu = algorithmic_bytes(D, K, thin, sink)
+    n_local = kern.n
+    frac = stored_fraction(burnin, thin, a.warmup + a.steps + 1, a.warmup + a.steps + min(a.steps, a.timing_steps))
+    bpu = algorithmic_bytes(D, K, frac, sink)
     if timing:
         kern.set_timing(True)
         n_t = min(a.steps, a.timing_steps)
@@ -211,36 +239,39 @@ def main():
         kern.set_timing(False)
         if kt["sweep_launches"]:
             t_launch = kt["sweep_ms"] / kt["sweep_launches"] * 1e-3
-            achieved = bpu * chains * n_per_rank / t_launch / 1e9
+            achieved = bpu * chains * n_local / t_launch / 1e9
             roofline = dict(bound="hbm", achieved=round(achieved, 3), peak=HBM_PEAK_GBS, unit="GB/s",
-                            frac=round(achieved / HBM_PEAK_GBS, 6), traffic=committed_traffic(a.workload, world),
-                            kernel="sweep_kernel (incl. fused level-2 tail)" if world == 1 else "sweep_kernel",
-                            bytes_per_unit=bpu, units_per_launch=chains * n_per_rank,
+                            frac=round(achieved / HBM_PEAK_GBS, 6), traffic=committed_traffic(a.workload, sharded),
+                            kernel="sweep_kernel (incl. fused level-2 tail)" if not sharded else "sweep_kernel",
+                            bytes_per_unit=round(bpu, 3), units_per_launch=chains * n_local,
                             sweep_kernel_us=round(t_launch * 1e6, 3), timed_launches=kt["sweep_launches"])
             if kt["hyper_launches"]:
                 roofline["hyper_kernel_us"] = round(kt["hyper_ms"] / kt["hyper_launches"] * 1e3, 3)
 
     if rank == 0:
         cpu = None
-        if world == 1 and not a.no_cpu_baseline:
+        if world == 1 and not a.no_cpu_baseline and not a.force_sharded:
             cpu = cpu_baseline(a.workload)
         wl = WORKLOADS[a.workload]
         line = dict(
             metric="MCMC sweeps/sec x N_customers (customer-sweeps/s)", value=value, unit="customer-sweeps/s",
             n_gpus=world, steps=a.steps, warmup=a.warmup, ms_per_step=dt / a.steps * 1e3, higher_is_better=True,
             scaling="weak", vs_baseline=None, dtype="f64",
-            data="CDNOW full CBS (23,570 real customers, tests/golden/cdnow_full_cbs.npz)"
-                 + ("" if world == 1 else f", tiled x{world} (one copy per rank)"),
+            data=(f"synthetic CBS ({n_total} customers, mcmc_clv_model_amd.data.synthetic_cbs)"
+                  if WORKLOADS[a.workload][1].startswith("synthetic:") else
+                  (f"CDNOW {WORKLOADS[a.workload][1]} CBS ({n_total // world:,} real customers, "
+                   f"tests/golden/cdnow_{WORKLOADS[a.workload][1]}_cbs.npz)")
+                  + ("" if world == 1 else f", tiled x{world} (one copy per rank)")),
             config=dict(workload=f"{a.workload}: {'bivariate' if D == 2 else 'trivariate'} M2, covariates {covs}",
-                        n_customers=n_per_rank * world, chains=chains, n_mh_steps=20, burnin=burnin, mcmc=mcmc,
+                        n_customers=n_total, chains=chains, n_mh_steps=20, burnin=burnin, mcmc=mcmc,
                         thin=thin, seed=42, draw_sink=sink, parallelism=f"customer-shard x{world}",
-                        timed_region="hipGraph replay of fused sweep launches" if world == 1 else
-                        "sweep + RCCL all_gather + level-2 launches per step"),
+                        timed_region="hipGraph replay of fused sweep launches" if not sharded else
+                        "per step: sweep + group kernels, RCCL all_gather, level-2 kernel"),
             roofline=roofline, cpu_baseline=cpu,
             speedup_vs_cpu_1core=(value / cpu["value"]) if cpu else None,
         )
         print(json.dumps(line))
-    kern.close() if world == 1 else ss.close()
+    kern.close() if not sharded else ss.close()
     if dist:
         dist.destroy_process_group()
 

@@ -17,7 +17,7 @@ except Exception:  # pragma: no cover - torch is optional for the single-GPU pat
     torch = None
 
 LIB_NAME = "libclvmcmc.so"
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+LIB_PATH = os.environ.get("CLV_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
 ABI_VERSION = 1
 BLOCK = 256
@@ -103,6 +103,7 @@ def lib() -> ctypes.CDLL:
                                          POINTER(c_float), POINTER(c_float), dp, dp, dp, dp]),
         "clv_debug_level2": (c_int32, [c_int32, c_int32, POINTER(ClvPrior), dp, dp, dp, dp, dp, dp, dp]),
         "clv_debug_hyper_variates": (c_int32, [c_uint64, c_int32, c_uint32, c_double, c_int64, dp, dp]),
+        "clv_debug_stamps": (c_int32, [sp, POINTER(c_uint64)]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(L, name)

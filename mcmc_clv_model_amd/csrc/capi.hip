@@ -60,6 +60,7 @@ struct clv_sampler {
   Ctrl* d_ctrl = nullptr;
   uint32_t* d_arrive = nullptr;     // [chain] fused-tail arrival counters
   double* d_hvar = nullptr;         // [chain][HV] precomputed hyper variates
+  unsigned long long* d_stamps = nullptr;  // CLV_STAMPS diagnostic build only
   double *d_level1 = nullptr, *d_level2 = nullptr, *d_loglik = nullptr, *d_sums = nullptr;
   double* d_tape = nullptr;
   double* d_bs = nullptr;  // staging for set_hyper
@@ -108,6 +109,7 @@ SweepArgs sweep_args(clv_sampler* s, int init, int fuse = 0) {
   a.fuse = fuse;
   a.chain_arrive = s->d_arrive;
   a.hvar_out = s->d_hvar;
+  a.stamps = s->d_stamps;
   a.h = hyper_args(s, nullptr, 0);
   if (fuse) a.h.hvar = s->replay ? nullptr : s->d_hvar;
   return a;
@@ -355,6 +357,14 @@ int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* pri
   CLV_HIPC(dalloc(&s->d_ctrl, 1));
   CLV_HIPC(dalloc(&s->d_arrive, C));
   CLV_HIPC(dalloc(&s->d_hvar, C * HV));
+#ifdef CLV_STAMPS
+  {
+    std::vector<unsigned long long> st(1024 * 8, 0ull);
+    for (int i = 0; i < 1024; ++i) st[i * 8 + 0] = st[i * 8 + 4] = ~0ull;
+    CLV_HIPC(dalloc(&s->d_stamps, st.size()));
+    CLV_HIPC(hipMemcpy(s->d_stamps, st.data(), st.size() * sizeof(unsigned long long), hipMemcpyHostToDevice));
+  }
+#endif
   CLV_HIPC(hipMemsetAsync(s->d_hvar, 0, sizeof(double) * C * HV, s->stream));
   CLV_HIPC(hipMemsetAsync(s->d_arrive, 0, sizeof(uint32_t) * C, s->stream));
   CLV_HIPC(dalloc(&s->d_bs, C * (CLV_MAX_K * CLV_MAX_D + CLV_MAX_D * CLV_MAX_D)));
@@ -436,7 +446,7 @@ void clv_destroy(clv_sampler* s) {
   for (auto e : s->ev) (void)hipEventDestroy(e);
   void* ptrs[] = {s->d_x, s->d_tx, s->d_T, s->d_cov, s->d_logs, s->d_lam, s->d_mu, s->d_hyper,
                   s->d_block, s->d_prior, s->d_ctrl, s->d_level1, s->d_level2, s->d_loglik,
-                  s->d_sums, s->d_tape, s->d_bs, s->d_arrive, s->d_hvar};
+                  s->d_sums, s->d_tape, s->d_bs, s->d_arrive, s->d_hvar, s->d_stamps};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (s->d_unit && s->d_unit != s->d_block) (void)hipFree(s->d_unit);
@@ -671,6 +681,14 @@ int clv_kernel_time(clv_sampler* s, double* sweep_ms, int64_t* n_sweep, double* 
 }
 
 // ---- test hooks ----
+int clv_debug_stamps(clv_sampler* s, uint64_t* out) {
+  if (!s || !out) return fail(CLV_EINVAL, "null argument");
+  if (!s->d_stamps) return fail(CLV_ESTATE, "library not built with CLV_STAMPS (make STAMPS=1)");
+  CLV_HIP(hipStreamSynchronize(s->stream));
+  CLV_HIP(hipMemcpy(out, s->d_stamps, sizeof(uint64_t) * 1024 * 8, hipMemcpyDeviceToHost));
+  return CLV_OK;
+}
+
 int clv_debug_philox(uint32_t k0, uint32_t k1, const uint32_t* ctr, int64_t n, uint32_t* out) {
   if (!ctr || !out || n < 0) return fail(CLV_EINVAL, "bad arguments");
   uint32_t *dc = nullptr, *dout = nullptr;

@@ -94,6 +94,7 @@ struct SweepArgs {
   double* hvar_out;          // [chain][HV]: the chain's last workgroup precomputes the next level-2
                              // draw's Philox variates at its start (off the critical path), or null
   HyperArgs h;               // level-2 arguments of the fused tail
+  unsigned long long* stamps; // diagnostic build only (CLV_STAMPS): [1024][8] s_memrealtime stamps
 };
 
 struct GroupArgs {

@@ -70,6 +70,22 @@ __device__ __forceinline__ void block_reduce(double (&v)[NS], double (*red)[NS],
 }
 
 // bi:402 (the reference's loop ends at burnin + mcmc, bi:383, so nothing beyond is stored)
+#ifdef CLV_STAMPS
+// Diagnostic build only: s_memrealtime (100 MHz) stamps per launch, slot = sweep % 1024:
+// [0] first block start (min) [1] last block end of customer work (max) [2] tail start (max)
+// [3] tail end (max) [4] first block end (min) [5] last block start (max)
+__device__ __forceinline__ void stamp(unsigned long long* st, int64_t s, int k, bool is_min) {
+  if (!st) return;
+  const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+  unsigned long long* p = st + (s & 1023) * 8 + k;
+  if (is_min) __hip_atomic_fetch_min(p, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else __hip_atomic_fetch_max(p, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+#define CLV_STAMP(st, s, k, is_min) stamp(st, s, k, is_min)
+#else
+#define CLV_STAMP(st, s, k, is_min) ((void)0)
+#endif
+
 __device__ __forceinline__ bool is_stored(int64_t s, const Geometry& g) {
   return s > g.burnin && s <= (int64_t)g.burnin + g.mcmc && ((s - 1 - g.burnin) % g.thin) == 0;
 }
@@ -291,31 +307,7 @@ __device__ void hyper_body(const HyperArgs& a, int c, int64_t s, int mode, const
   const int tid = threadIdx.x;
   const int64_t hs = (D == 2) ? s + 1 : s;  // sweep the drawn (beta, Sigma) belongs to
 
-  // 1. fixed-order reduction over all units of all shards (independent of world size)
-  double acc[NS];
-#pragma unroll
-  for (int j = 0; j < NS; ++j) acc[j] = 0.0;
-  for (int64_t u = tid; u < g.n_units_global; u += 256) {
-    if (blocks) {  // world_size == 1: units formed from this chain's block partials
-      const double* p = blocks + ((int64_t)c * g.blocks_per_rank + u * g.blocks_per_unit) * g.stride;
-#pragma unroll
-      for (int j = 0; j < NS; ++j) {
-        double t = 0.0;
-        for (int bb = 0; bb < g.blocks_per_unit; ++bb)
-          t += __hip_atomic_load(p + (int64_t)bb * g.stride + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        acc[j] += t;
-      }
-    } else {
-      const int64_t r = u / g.units_per_rank;
-      const int64_t lu = u - r * g.units_per_rank;
-      const double* p = a.units + ((r * g.n_chains + c) * g.units_per_rank + lu) * g.stride;
-#pragma unroll
-      for (int j = 0; j < NS; ++j) acc[j] += p[j];
-    }
-  }
-  block_reduce<NS>(acc, red, tot);
-
-  // 2. variates
+  // 1. variates first: independent of the statistics, so their loads overlap the reduction's
   if constexpr (REPLAY) {
     const double* tv = a.r.tape + ((int64_t)c * a.r.tape_sweeps + (hs - 1)) * a.r.tape_sweep_stride +
                        (a.r.tape_sweep_stride - TAPE_HYPER);
@@ -338,7 +330,29 @@ __device__ void hyper_body(const HyperArgs& a, int c, int64_t s, int mode, const
       var_chi[q] = chi2_draw(k0, k1, (uint32_t)hs, q, a.nu_n - D + 1 + q);
     }
   }
-  __syncthreads();
+  // 2. fixed-order reduction over all units of all shards (independent of world size)
+  double acc[NS];
+#pragma unroll
+  for (int j = 0; j < NS; ++j) acc[j] = 0.0;
+  for (int64_t u = tid; u < g.n_units_global; u += 256) {
+    if (blocks) {  // world_size == 1: units formed from this chain's block partials
+      const double* p = blocks + ((int64_t)c * g.blocks_per_rank + u * g.blocks_per_unit) * g.stride;
+#pragma unroll
+      for (int j = 0; j < NS; ++j) {
+        double t = 0.0;
+        for (int bb = 0; bb < g.blocks_per_unit; ++bb)
+          t += __hip_atomic_load(p + (int64_t)bb * g.stride + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        acc[j] += t;
+      }
+    } else {
+      const int64_t r = u / g.units_per_rank;
+      const int64_t lu = u - r * g.units_per_rank;
+      const double* p = a.units + ((r * g.n_chains + c) * g.units_per_rank + lu) * g.stride;
+#pragma unroll
+      for (int j = 0; j < NS; ++j) acc[j] += p[j];
+    }
+  }
+  block_reduce<NS>(acc, red, tot);  // its barriers also publish the variates written to LDS above
 
   // 3. algebra + outputs (one lane)
   if (tid == 0) {
@@ -404,6 +418,10 @@ __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
   double acc[NS];
 #pragma unroll
   for (int j = 0; j < NS; ++j) acc[j] = 0.0;
+  if (threadIdx.x == 0 && !a.init) {
+    CLV_STAMP(a.stamps, s, 0, true);
+    CLV_STAMP(a.stamps, s, 5, false);
+  }
 
   // ---- the next level-2 draw's Philox variates (independent of the statistics): computed by
   // wave 3 of the chain's last workgroup — the partially filled one — so the draw's serial
@@ -538,13 +556,12 @@ __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
         // accept/reject chain runs (ILP for the ~1.5 waves/SIMD of the CDNOW-sized problem).
         constexpr int MC = MH_CHUNK;
         float tl[MC], tm[MC], lu[MC];
+        const SlotPhilox ph(k0, k1, gi, (uint32_t)s);
         auto gen = [&](int j0, float (&a)[MC], float (&b)[MC], float (&c)[MC]) {
 #pragma unroll
           for (int q = 0; q < MC; ++q) {
             const uint32_t j = (uint32_t)(j0 + q);
-            const u32x4 ra = customer_block(k0, k1, gi, (uint32_t)s, SLOT_MH0 + 2u * j);
-            const u32x4 rb = customer_block(k0, k1, gi, (uint32_t)s, SLOT_MH0 + 2u * j + 1u);
-            mh_variates(ra, rb, &a[q], &b[q], &c[q]);
+            mh_variates(ph(SLOT_MH0 + 2u * j), ph(SLOT_MH0 + 2u * j + 1u), &a[q], &b[q], &c[q]);
           }
         };
         auto step = [&](float t_l, float t_m, float l_u) {
@@ -572,10 +589,8 @@ __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
           }
         }
         for (int j = S_full; j < g.S; ++j) {  // remainder steps
-          const u32x4 ra = customer_block(k0, k1, gi, (uint32_t)s, SLOT_MH0 + 2u * j);
-          const u32x4 rb = customer_block(k0, k1, gi, (uint32_t)s, SLOT_MH0 + 2u * j + 1u);
           float a1, b1, c1;
-          mh_variates(ra, rb, &a1, &b1, &c1);
+          mh_variates(ph(SLOT_MH0 + 2u * j), ph(SLOT_MH0 + 2u * j + 1u), &a1, &b1, &c1);
           step(a1, b1, c1);
         }
       }
@@ -670,6 +685,8 @@ __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
+      CLV_STAMP(a.stamps, s, 1, false);
+      CLV_STAMP(a.stamps, s, 4, true);
       const uint32_t old = __hip_atomic_fetch_add(a.chain_arrive + c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const uint32_t last = old == (uint32_t)(g.nb_local - 1) ? 1u : 0u;
       if (last) __hip_atomic_store(a.chain_arrive + c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -677,7 +694,11 @@ __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
     }
     __syncthreads();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only
-    if (s_last) hyper_body<D, K, REPLAY, NS>(a.h, c, s, 0, a.blockpart, red, tot, var_iw, var_chi, var_noise);
+    if (s_last) {
+      if (threadIdx.x == 0) CLV_STAMP(a.stamps, s, 2, false);
+      hyper_body<D, K, REPLAY, NS>(a.h, c, s, 0, a.blockpart, red, tot, var_iw, var_chi, var_noise);
+      if (threadIdx.x == 0) CLV_STAMP(a.stamps, s, 3, false);
+    }
   }
 }
 
@@ -720,9 +741,10 @@ __global__ void debug_variates_kernel(uint64_t seed, int chain, uint32_t sweep, 
   ea[i] = -log(u53_open0(r.z, r.w));
   const u32x4 re = customer_block(k0, k1, (uint32_t)i, sweep, SLOT_ETA);
   ez[i] = sqrt(-2.0 * log(u53_open0(re.x, re.y))) * cospi(2.0 * u53(re.z, re.w));
+  const SlotPhilox ph(k0, k1, (uint32_t)i, sweep);
   for (int j = 0; j < S; ++j) {
-    const u32x4 ra = customer_block(k0, k1, (uint32_t)i, sweep, SLOT_MH0 + 2u * j);
-    const u32x4 rb = customer_block(k0, k1, (uint32_t)i, sweep, SLOT_MH0 + 2u * j + 1u);
+    const u32x4 ra = ph(SLOT_MH0 + 2u * j);
+    const u32x4 rb = ph(SLOT_MH0 + 2u * j + 1u);
     float a, b, lu;
     mh_variates(ra, rb, &a, &b, &lu);
     tl[(int64_t)j * n + i] = a;

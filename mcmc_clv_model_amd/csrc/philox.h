@@ -55,6 +55,44 @@ CLV_HD double u53_open0(uint32_t lo, uint32_t hi) {
 CLV_HD u32x4 customer_block(uint32_t k0, uint32_t k1, uint32_t customer, uint32_t sweep, uint32_t slot) {
   return philox4x32_10(u32x4{customer, sweep, slot, STREAM_CUSTOMER}, k0, k1);
 }
+
+// Philox4x32-10 of counter (customer, sweep, slot, STREAM_CUSTOMER) with the slot-independent
+// products hoisted: round 1's M0*customer and round 2's M1*(hi(M0*customer)^stream^k1) depend only
+// on (customer, key), so one sweep's blocks cost 18 instead of 20 multiplies.  Bit-identical to
+// customer_block() (checked by the device KAT test through clv_debug_variates).
+struct SlotPhilox {
+  uint32_t k0, k1, sweep;
+  uint32_t r1z, r1w;     // round-1 outputs that do not depend on the slot
+  uint64_t p1r2;         // round-2 product M1 * r1z
+  CLV_HD SlotPhilox(uint32_t k0_, uint32_t k1_, uint32_t customer, uint32_t sweep_) : k0(k0_), k1(k1_), sweep(sweep_) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * customer;
+    r1z = (uint32_t)(p0 >> 32) ^ STREAM_CUSTOMER ^ k1_;
+    r1w = (uint32_t)p0;
+    p1r2 = (uint64_t)0xCD9E8D57u * r1z;
+  }
+  CLV_HD u32x4 operator()(uint32_t slot) const {
+    // round 1 (key k)
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * slot;
+    u32x4 c{(uint32_t)(p1 >> 32) ^ sweep ^ k0, (uint32_t)p1, r1z, r1w};
+    uint32_t a0 = k0 + 0x9E3779B9u, a1 = k1 + 0xBB67AE85u;
+    // round 2: the second product is slot-independent
+    {
+      const uint64_t q0 = (uint64_t)0xD2511F53u * c.x;
+      c = u32x4{(uint32_t)(p1r2 >> 32) ^ c.y ^ a0, (uint32_t)p1r2, (uint32_t)(q0 >> 32) ^ c.w ^ a1, (uint32_t)q0};
+      a0 += 0x9E3779B9u;
+      a1 += 0xBB67AE85u;
+    }
+#pragma unroll
+    for (int r = 2; r < 10; ++r) {
+      const uint64_t q0 = (uint64_t)0xD2511F53u * c.x;
+      const uint64_t q1 = (uint64_t)0xCD9E8D57u * c.z;
+      c = u32x4{(uint32_t)(q1 >> 32) ^ c.y ^ a0, (uint32_t)q1, (uint32_t)(q0 >> 32) ^ c.w ^ a1, (uint32_t)q0};
+      a0 += 0x9E3779B9u;
+      a1 += 0xBB67AE85u;
+    }
+    return c;
+  }
+};
 CLV_HD u32x4 hyper_block(uint32_t k0, uint32_t k1, uint32_t slot, uint32_t sweep) {
   return philox4x32_10(u32x4{slot, sweep, 0u, STREAM_HYPER}, k0, k1);
 }

@@ -196,3 +196,15 @@ def test_shard_plan_covers_and_aligns(world):
         assert p.blocks_per_rank % p.blocks_per_unit == 0
         assert p.blocks_per_unit == D.default_blocks_per_unit(n)  # world-independent unit size
         assert p.units_per_rank * world >= p.n_units_global
+
+
+def test_philox_header_host_build_kat_and_hoisting(tmp_path):
+    """csrc/philox.h compiled for the host with g++: Random123 KATs and SlotPhilox (hoisted
+    slot-independent products, used by the sweep kernel) bit-identical to plain Philox4x32-10."""
+    import subprocess
+    src = os.path.join(os.path.dirname(os.path.abspath(__file__)), "cpp", "philox_host_check.cpp")
+    exe = str(tmp_path / "philox_check")
+    subprocess.run(["g++", "-O2", "-std=c++17", src, "-o", exe], check=True)
+    out = subprocess.run([exe], capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "mismatches 0" in out.stdout

@@ -1,0 +1,47 @@
+#!/usr/bin/env python
+"""Where does a sweep launch spend its time?  Runs a workload on the diagnostic library
+(libclvmcmc_stamps.so: `make -C mcmc_clv_model_amd/csrc STAMPS=1`) and reports, per launch, the
+medians of the in-kernel s_memrealtime stamps (100 MHz):
+  customer phase  = last workgroup's end of customer work - first workgroup start
+  first/last      = first workgroup end, last workgroup start (relative to first start)
+  ticket->tail    = last ticket -> tail start;  tail = fused level-2 draw duration
+Diagnostic only: the stamps' atomics perturb the kernel slightly; read shares, not absolutes.
+"""
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ.setdefault("CLV_LIB_PATH", os.path.join(ROOT, "mcmc_clv_model_amd", "libclvmcmc_stamps.so"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+
+def main(workload="c2", sweeps=1500, chains=None):
+    import bench
+    from mcmc_clv_model_amd.sampler import HipSampler, build_problem
+    df, D, covs, ch, burnin, mcmc, thin, sink = bench.load_workload(workload)
+    p = build_problem(df, covs, D)
+    s = HipSampler(p, mcmc=mcmc, burnin=burnin, thin=thin, chains=chains or ch, seed=42, draw_sink=sink)
+    s.run(sweeps)
+    st = np.zeros(1024 * 8, np.uint64)
+    rc = s._L.clv_debug_stamps(s.h, st.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)))
+    assert rc == 0, s._L.clv_last_error()
+    st = st.reshape(1024, 8).astype(np.int64)
+    ok = (st[:, 3] > 0) & (st[:, 0] > 0)
+    st = st[ok]
+    us = lambda a: np.median(a) * 0.01  # noqa: E731  (10 ns ticks -> us)
+    rel = st - st[:, :1]
+    print(f"{workload}: {ok.sum()} launches, chains={chains or ch}, N={len(df)}")
+    print(f"  launch total (first start -> tail end): {us(rel[:, 3]):8.2f} us")
+    print(f"  customer phase (-> last block end):     {us(rel[:, 1]):8.2f} us")
+    print(f"  first block end:                        {us(rel[:, 4]):8.2f} us")
+    print(f"  last block start:                       {us(rel[:, 5]):8.2f} us")
+    print(f"  last block end -> tail start:           {us(st[:, 2] - st[:, 1]):8.2f} us")
+    print(f"  tail (level-2 draw):                    {us(st[:, 3] - st[:, 2]):8.2f} us")
+    s.close()
+
+
+if __name__ == "__main__":
+    main(*(sys.argv[1:2] or ["c2"]), *(int(x) for x in sys.argv[2:]))
