@@ -150,6 +150,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true", help="skip the event-timed roofline pass")
     ap.add_argument("--timing-steps", type=int, default=3000, help="sweeps in the event-timed roofline pass")
+    ap.add_argument("--graph-chunk", type=int, default=32,
+                    help="sharded path: sweeps (incl. the RCCL all-gather) per captured torch.cuda graph; 0 = eager")
     ap.add_argument("--force-sharded", action="store_true",
                     help="use the sharded path (torch.distributed exchange) even at world size 1")
     ap.add_argument("--cpu-baseline-child", action="store_true")
@@ -197,10 +199,10 @@ def main():
         from mcmc_clv_model_amd.distributed import ShardedSampler
         p = build_problem(df, covs, D)
         ss = ShardedSampler(p, rank=rank, world=world, chains=chains, mcmc=mcmc, burnin=burnin, thin=thin, seed=42,
-                            draw_sink=sink, device=local_rank)
+                            draw_sink=sink, device=local_rank, graph_chunk=a.graph_chunk)
         run = ss.step
         sync = ss.synchronize
-        kern = ss.s
+        kern = ss
 
     K = len(covs) + 1
     timing = not a.no_kernel_timing
@@ -266,12 +268,13 @@ def main():
                         n_customers=n_total, chains=chains, n_mh_steps=20, burnin=burnin, mcmc=mcmc,
                         thin=thin, seed=42, draw_sink=sink, parallelism=f"customer-shard x{world}",
                         timed_region="hipGraph replay of fused sweep launches" if not sharded else
-                        "per step: sweep + group kernels, RCCL all_gather, level-2 kernel"),
+                        f"torch.cuda graph replay ({a.graph_chunk} sweeps: sweep + group kernels, RCCL all_gather, "
+                        "level-2 kernel)" if a.graph_chunk else "eager: sweep + group kernels, RCCL all_gather, level-2"),
             roofline=roofline, cpu_baseline=cpu,
             speedup_vs_cpu_1core=(value / cpu["value"]) if cpu else None,
         )
         print(json.dumps(line))
-    kern.close() if not sharded else ss.close()
+    kern.close()
     if dist:
         dist.destroy_process_group()
 

@@ -135,6 +135,11 @@ int clv_partials(clv_sampler* s, double** device_ptr, int64_t* n_doubles, int32_
 int clv_copy_partials(clv_sampler* s, void* dst_device_ptr);
 int clv_synchronize(clv_sampler* s);
 int64_t clv_sweeps_done(const clv_sampler* s);
+/* Launch on another stream from now on (e.g. a stream under hipGraph capture by the caller,
+ * who then replays the captured sweeps), and adjust the host's sweep count by n (+chunk per
+ * replay; -chunk after a capture, which records launches without executing them). */
+int clv_set_stream(clv_sampler* s, uint64_t stream);
+int clv_note_sweeps(clv_sampler* s, int64_t n);
 
 /* Outputs. level1: [chain][draw][n][D+2] (lambda, mu, tau, z, [eta]) — bi:407-410, tri:544-548;
  * level2: [chain][draw][D*K + D(D+1)/2] — bi:411-412, tri:549-554;

@@ -50,6 +50,7 @@ struct clv_sampler {
   bool replay = false;
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t own = nullptr;  // stream created by the sampler (destroyed with it)
   bool own_stream = false;
 
   int32_t* d_x = nullptr;
@@ -338,6 +339,7 @@ int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* pri
     s->stream = (hipStream_t)(uintptr_t)cfg->stream;
   } else {
     CLV_HIPC(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+    s->own = s->stream;
     s->own_stream = true;
   }
 
@@ -450,7 +452,7 @@ void clv_destroy(clv_sampler* s) {
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (s->d_unit && s->d_unit != s->d_block) (void)hipFree(s->d_unit);
-  if (s->own_stream && s->stream) (void)hipStreamDestroy(s->stream);
+  if (s->own_stream && s->own) (void)hipStreamDestroy(s->own);
   delete s;
 }
 
@@ -533,6 +535,22 @@ int clv_synchronize(clv_sampler* s) {
 }
 
 int64_t clv_sweeps_done(const clv_sampler* s) { return s ? s->sweeps_done : -1; }
+
+int clv_set_stream(clv_sampler* s, uint64_t stream) {
+  if (!s || !stream) return fail(CLV_EINVAL, "bad arguments");
+  if (s->graph_exec) {
+    CLV_HIP(hipGraphExecDestroy(s->graph_exec));  // captured on the previous stream
+    s->graph_exec = nullptr;
+  }
+  s->stream = (hipStream_t)(uintptr_t)stream;  // caller-owned from now on
+  return CLV_OK;
+}
+
+int clv_note_sweeps(clv_sampler* s, int64_t n) {
+  if (!s || s->sweeps_done + n < 0) return fail(CLV_EINVAL, "bad arguments");
+  s->sweeps_done += n;
+  return CLV_OK;
+}
 
 int clv_run(clv_sampler* s, int64_t n_sweeps) {
   if (!s) return fail(CLV_EINVAL, "null sampler");

@@ -84,10 +84,17 @@ def exchange(local, gathered, group=None) -> None:
 
 
 class ShardedSampler:
-    """This rank's shard of a problem on its GPU; sweeps with one all-gather per sweep."""
+    """This rank's shard of a problem on its GPU; sweeps with one all-gather per sweep.
+
+    ``graph_chunk`` > 0 captures that many sweeps (kernels, partial copy, RCCL all-gather) into a
+    torch.cuda.CUDAGraph on first use and replays it; the sweep index lives in device memory, so
+    one graph serves every chunk and the host issues one replay per chunk instead of ~5 calls per
+    sweep.
+    """
 
     def __init__(self, p_global, *, rank: int, world: int, chains: int, mcmc: int, burnin: int, thin: int,
-                 seed: int, n_mh_steps: int = 20, draw_sink: str = "summary", device: int = 0, group=None):
+                 seed: int, n_mh_steps: int = 20, draw_sink: str = "summary", device: int = 0, group=None,
+                 graph_chunk: int = 0):
         import torch
         from .sampler import HipSampler, make_prior
         self.torch = torch
@@ -95,34 +102,79 @@ class ShardedSampler:
         b, e = self.plan.shard(rank)
         self.begin, self.end = b, e
         self.rank, self.world, self.group = rank, world, group
+        self.graph_chunk, self.graph, self.timing = int(graph_chunk), None, False
         torch.cuda.set_device(device)
-        stream = torch.cuda.current_stream().cuda_stream
+        # One explicit stream carries the sampler's launches AND the exchange (copy, all-gather):
+        # a sampler-owned non-blocking stream would not be ordered against torch's default stream.
+        self.stream = torch.cuda.Stream(device=device)
+        self.base_stream = self.stream.cuda_stream
         prior = make_prior(p_global, p_global.N)
         self.s = HipSampler(slice_problem(p_global, b, e), mcmc=mcmc, burnin=burnin, thin=thin, chains=chains,
                             seed=seed, n_mh_steps=n_mh_steps, draw_sink=draw_sink, device=device,
                             n_global=p_global.N, shard_begin=rank * self.plan.blocks_per_rank * BLOCK,
                             world_size=world, rank=rank, blocks_per_rank=self.plan.blocks_per_rank,
-                            blocks_per_unit=self.plan.blocks_per_unit, stream=stream, prior=prior)
+                            blocks_per_unit=self.plan.blocks_per_unit, stream=self.base_stream, prior=prior)
+        self.n = self.s.n
         _, nd, _ = self.s.partials()
         self.local = torch.zeros(nd, dtype=torch.float64, device=f"cuda:{device}")
         self.gathered = torch.zeros(nd * world, dtype=torch.float64, device=f"cuda:{device}")
+        self.cur = self.stream  # the stream launches go to (a capture stream while capturing)
         self.D = p_global.D
         if self.D == 2:  # bivariate: the draw for sweep 1 comes from the initial state (bi:393)
             self._exchange_and_hyper()
 
     def _exchange_and_hyper(self) -> None:
         self.s.copy_partials(self.local.data_ptr())
-        exchange(self.local, self.gathered, self.group)
+        with self.torch.cuda.stream(self.cur):
+            exchange(self.local, self.gathered, self.group)
         self.s.hyper(self.gathered.data_ptr())
 
-    def step(self, n: int = 1) -> None:
+    def _eager(self, n: int) -> None:
         for _ in range(n):
             self.s.sweep()
             self._exchange_and_hyper()
+
+    def step(self, n: int = 1) -> None:
+        torch = self.torch
+        left = n
+        if self.graph_chunk and not self.timing:
+            if self.graph is None and left >= self.graph_chunk:
+                self._capture()
+            while self.graph is not None and left >= self.graph_chunk:
+                with torch.cuda.stream(self.stream):
+                    self.graph.replay()
+                self.s.note_sweeps(self.graph_chunk)
+                left -= self.graph_chunk
+        self._eager(left)
+
+    def _capture(self) -> None:
+        torch = self.torch
+        self.synchronize()
+        g = torch.cuda.CUDAGraph()
+        cap = torch.cuda.Stream(device=self.stream.device)
+        with torch.cuda.graph(g, stream=cap):
+            self.s.set_stream(cap.cuda_stream)
+            self.cur = cap
+            try:
+                self._eager(self.graph_chunk)
+            finally:
+                self.cur = self.stream
+        self.s.set_stream(self.base_stream)
+        self.s.note_sweeps(-self.graph_chunk)  # capture recorded the launches, it ran nothing
+        self.graph = g
+        torch.cuda.synchronize()
+
+    def set_timing(self, enable: bool) -> None:
+        self.timing = bool(enable)
+        self.s.set_timing(enable)
+
+    def kernel_time(self):
+        return self.s.kernel_time()
 
     def synchronize(self) -> None:
         self.s.synchronize()
         self.torch.cuda.synchronize()
 
     def close(self) -> None:
+        self.graph = None
         self.s.close()

@@ -203,6 +203,12 @@ class HipSampler:
         check(self._L.clv_partials(self.h, ctypes.byref(ptr), ctypes.byref(nd), ctypes.byref(st)))
         return ptr.value, nd.value, st.value
 
+    def set_stream(self, stream: int) -> None:
+        check(self._L.clv_set_stream(self.h, int(stream)))
+
+    def note_sweeps(self, n: int) -> None:
+        check(self._L.clv_note_sweeps(self.h, int(n)))
+
     def copy_partials(self, dst_ptr: int) -> None:
         check(self._L.clv_copy_partials(self.h, ctypes.c_void_p(dst_ptr)))
 
