@@ -18,7 +18,6 @@
 
 namespace clv {
 
-constexpr int MH_CHUNK = 4;  // MH steps whose variates are generated one chunk ahead
 
 __device__ __forceinline__ double clip70(double v) {  // np.clip(v, -70, 70), NaN passes (bi:323)
   return v < -70.0 ? -70.0 : (v > 70.0 ? 70.0 : v);
@@ -551,19 +550,12 @@ __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
           }
         }
       } else {
-        // Software pipeline: the Philox blocks and t3 transforms of the next MH_CHUNK steps are
-        // independent of the state, so they are generated while the current chunk's fp64
+        // Software pipeline: the Philox blocks and t3 transforms of the next chunk of 4 MH steps
+        // are independent of the state, so they are generated while the current chunk's fp64
         // accept/reject chain runs (ILP for the ~1.5 waves/SIMD of the CDNOW-sized problem).
-        constexpr int MC = MH_CHUNK;
+        constexpr int MC = MH_CHUNK_STEPS;
         float tl[MC], tm[MC], lu[MC];
         const SlotPhilox ph(k0, k1, gi, (uint32_t)s);
-        auto gen = [&](int j0, float (&a)[MC], float (&b)[MC], float (&c)[MC]) {
-#pragma unroll
-          for (int q = 0; q < MC; ++q) {
-            const uint32_t j = (uint32_t)(j0 + q);
-            mh_variates(ph(SLOT_MH0 + 2u * j), ph(SLOT_MH0 + 2u * j + 1u), &a[q], &b[q], &c[q]);
-          }
-        };
         auto step = [&](float t_l, float t_m, float l_u) {
           const double pl = clip70(ll + s00 * (double)t_l);
           const double pm = clip70(lm + s11 * (double)t_m);
@@ -574,24 +566,20 @@ __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
             cur = plp;
           }
         };
-        const int S_full = g.S - g.S % MC;
-        if (S_full > 0) gen(0, tl, tm, lu);
-        for (int j0 = 0; j0 < S_full; j0 += MC) {
+        const int n_chunks = (g.S + MC - 1) / MC;
+        if (n_chunks > 0) mh_chunk_variates(ph, 0u, tl, tm, lu);
+        for (int q = 0; q < n_chunks; ++q) {
           float ntl[MC], ntm[MC], nlu[MC];
-          if (j0 + MC < S_full) gen(j0 + MC, ntl, ntm, nlu);
+          if (q + 1 < n_chunks) mh_chunk_variates(ph, (uint32_t)(q + 1), ntl, ntm, nlu);
 #pragma unroll
-          for (int q = 0; q < MC; ++q) step(tl[q], tm[q], lu[q]);
+          for (int i = 0; i < MC; ++i)
+            if (q * MC + i < g.S) step(tl[i], tm[i], lu[i]);  // uniform guard: last chunk may be partial
 #pragma unroll
-          for (int q = 0; q < MC; ++q) {
-            tl[q] = ntl[q];
-            tm[q] = ntm[q];
-            lu[q] = nlu[q];
+          for (int i = 0; i < MC; ++i) {
+            tl[i] = ntl[i];
+            tm[i] = ntm[i];
+            lu[i] = nlu[i];
           }
-        }
-        for (int j = S_full; j < g.S; ++j) {  // remainder steps
-          float a1, b1, c1;
-          mh_variates(ph(SLOT_MH0 + 2u * j), ph(SLOT_MH0 + 2u * j + 1u), &a1, &b1, &c1);
-          step(a1, b1, c1);
         }
       }
       lam = exp(ll);  // bi:337-338
@@ -742,14 +730,18 @@ __global__ void debug_variates_kernel(uint64_t seed, int chain, uint32_t sweep, 
   const u32x4 re = customer_block(k0, k1, (uint32_t)i, sweep, SLOT_ETA);
   ez[i] = sqrt(-2.0 * log(u53_open0(re.x, re.y))) * cospi(2.0 * u53(re.z, re.w));
   const SlotPhilox ph(k0, k1, (uint32_t)i, sweep);
-  for (int j = 0; j < S; ++j) {
-    const u32x4 ra = ph(SLOT_MH0 + 2u * j);
-    const u32x4 rb = ph(SLOT_MH0 + 2u * j + 1u);
-    float a, b, lu;
-    mh_variates(ra, rb, &a, &b, &lu);
-    tl[(int64_t)j * n + i] = a;
-    tm[(int64_t)j * n + i] = b;
-    ua[(int64_t)j * n + i] = uf32(rb.z);
+  for (int q = 0; q * MH_CHUNK_STEPS < S; ++q) {
+    float a[4], b[4], lu[4];
+    mh_chunk_variates(ph, (uint32_t)q, a, b, lu);
+    for (int k = 0; k < MH_CHUNK_STEPS && q * MH_CHUNK_STEPS + k < S; ++k) {
+      const int j = q * MH_CHUNK_STEPS + k;
+      const int w = MH_WORDS * j + 4;  // accept-uniform word of step j
+      const u32x4 r = ph(SLOT_MH0 + (uint32_t)(w / 4));
+      const uint32_t wa = (w % 4 == 0) ? r.x : (w % 4 == 1) ? r.y : (w % 4 == 2) ? r.z : r.w;
+      tl[(int64_t)j * n + i] = a[k];
+      tm[(int64_t)j * n + i] = b[k];
+      ua[(int64_t)j * n + i] = uf32(wa);
+    }
   }
 }
 

@@ -74,10 +74,24 @@ def hyper_block(seed, chain, slot, sweep):
     return philox4x32_10(np.array([slot, sweep, 0, STREAM_HYPER], dtype=np.uint32), k0, k1)
 
 
-def box_muller_f32(a, b):
-    r = np.sqrt(np.float32(-2.0) * np.log(uf32(a)))
-    t = uf32(b).astype(np.float64) * (2.0 * np.pi)
-    return (r * np.cos(t)).astype(np.float32), (r * np.sin(t)).astype(np.float32)
+def t3_f32(wu, wv):
+    """Student-t(3) by Bailey's trigonometric polar form: sqrt(3 (U^(-2/3) - 1)) cos(2 pi V)
+    (csrc/philox.h:t3_f32; fp32 like the device's v_log/v_exp/v_sqrt/v_cos)."""
+    p = np.exp2(np.float32(-2.0 / 3.0) * np.log2(uf32(wu))).astype(np.float32)
+    r = np.sqrt(np.float32(3.0) * (p - np.float32(1.0))).astype(np.float32)
+    return (r * np.cos(uf32(wv).astype(np.float64) * (2.0 * np.pi))).astype(np.float32)
+
+
+MH_WORDS, MH_CHUNK_STEPS, MH_CHUNK_BLOCKS = 5, 4, 5
+
+
+def mh_words(seed, chain, cust, sweep, n_steps):
+    """(5 * n_steps, n) uint32: the MH word stream, word w = lane w % 4 of block SLOT_MH0 + w // 4."""
+    n_blocks = -(-MH_WORDS * n_steps // 4)
+    w = np.empty((4 * n_blocks, len(cust)), np.uint32)
+    for b in range(n_blocks):
+        w[4 * b:4 * b + 4] = customer_blocks(seed, chain, cust, sweep, SLOT_MH0 + b).T
+    return w[:MH_WORDS * n_steps]
 
 
 def sweep_variates(seed, chain, sweep, n, n_steps):
@@ -88,20 +102,8 @@ def sweep_variates(seed, chain, sweep, n, n_steps):
                e_alive=-np.log(u53_open0(r[:, 2], r[:, 3])))
     re = customer_blocks(seed, chain, cust, sweep, SLOT_ETA)
     out["eta_z"] = np.sqrt(-2.0 * np.log(u53_open0(re[:, 0], re[:, 1]))) * np.cos(2.0 * np.pi * u53(re[:, 2], re[:, 3]))
-    tl = np.empty((n_steps, n), np.float32)
-    tm = np.empty((n_steps, n), np.float32)
-    ua = np.empty((n_steps, n), np.float32)
-    for j in range(n_steps):
-        ra = customer_blocks(seed, chain, cust, sweep, SLOT_MH0 + 2 * j)
-        rb = customer_blocks(seed, chain, cust, sweep, SLOT_MH0 + 2 * j + 1)
-        za, zb = box_muller_f32(ra[:, 0], ra[:, 1])
-        zc, zd = box_muller_f32(rb[:, 0], rb[:, 1])
-        chi_l = zc * zc + np.float32(-2.0) * np.log(uf32(ra[:, 2]))
-        chi_m = zd * zd + np.float32(-2.0) * np.log(uf32(ra[:, 3]))
-        tl[j] = za / np.sqrt(chi_l / np.float32(3.0))
-        tm[j] = zb / np.sqrt(chi_m / np.float32(3.0))
-        ua[j] = uf32(rb[:, 2])
-    out.update(t_l=tl, t_m=tm, u_acc=ua)
+    w = mh_words(seed, chain, cust, sweep, n_steps).reshape(n_steps, MH_WORDS, n)
+    out.update(t_l=t3_f32(w[:, 0], w[:, 1]), t_m=t3_f32(w[:, 2], w[:, 3]), u_acc=uf32(w[:, 4]))
     return out
 
 

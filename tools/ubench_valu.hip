@@ -36,6 +36,14 @@ __global__ void kern(uint64_t* out, float* fo, double* dout, uint32_t seed) {
         f[i] = __builtin_fmaf(f[i], 0.999f, 1e-4f);
       } else if constexpr (OP == 6) {  // v_mul_hi_u32 only
         a[i] = __umulhi(a[i], 0xD2511F53u) ^ a[i];
+      } else if constexpr (OP == 7) {  // v_mul_u32_u24 + xor
+        a[i] = __umul24(a[i], 0x9F53u) ^ (a[i] >> 3);
+      } else if constexpr (OP == 8) {  // v_mul_lo_u32 + xor
+        a[i] = (a[i] * 0xD2511F53u) ^ (a[i] >> 3);
+      } else if constexpr (OP == 9) {  // v_add_f64
+        d[i] = d[i] + 1e-7;
+      } else if constexpr (OP == 10) {  // v_mul_f64
+        d[i] = d[i] * 0.9999999;
       }
     }
   }
@@ -87,5 +95,9 @@ int main() {
   run<2>("v_fma_f64", 1);
   run<3>("v_log_f32 + add", 2);
   run<4>("exp(double) ocml", 1);
+  run<7>("mul_u32_u24 + xor + shr", 3);
+  run<8>("mul_lo_u32 + xor + shr", 3);
+  run<9>("v_add_f64", 1);
+  run<10>("v_mul_f64", 1);
   return 0;
 }
