@@ -178,6 +178,8 @@ int clv_debug_stamps(clv_sampler* s, uint64_t* out);
 /* Philox-mode chi-square and normal draws of the hyper stream (n of each). */
 int clv_debug_hyper_variates(uint64_t seed, int32_t chain, uint32_t sweep, double df, int64_t n,
                              double* chi2, double* normals);
+/* The Philox-mode MH step's fp64 exp (csrc/fastmath.h, |x| <= 700) on n values. */
+int clv_debug_exp(const double* x, int64_t n, double* out);
 
 #ifdef __cplusplus
 }

@@ -795,4 +795,17 @@ int clv_debug_hyper_variates(uint64_t seed, int32_t chain, uint32_t sweep, doubl
   return CLV_OK;
 }
 
+int clv_debug_exp(const double* x, int64_t n, double* out) {
+  if (!x || !out || n < 1) return fail(CLV_EINVAL, "bad arguments");
+  double *dx, *dout;
+  CLV_HIP(dalloc(&dx, n));
+  CLV_HIP(dalloc(&dout, n));
+  CLV_HIP(hipMemcpy(dx, x, sizeof(double) * n, hipMemcpyHostToDevice));
+  CLV_HIP(launch_debug_exp(dx, n, dout, nullptr));
+  CLV_HIP(hipMemcpy(out, dout, sizeof(double) * n, hipMemcpyDeviceToHost));
+  CLV_HIP(hipFree(dx));
+  CLV_HIP(hipFree(dout));
+  return CLV_OK;
+}
+
 }  // extern "C"

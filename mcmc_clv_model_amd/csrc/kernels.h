@@ -120,5 +120,6 @@ hipError_t launch_debug_level2(int D, int K, const double* prior_dev, const doub
                                hipStream_t st);
 hipError_t launch_debug_hyper_variates(uint64_t seed, int chain, uint32_t sweep, double df, int64_t n,
                                        double* chi2, double* normals, hipStream_t st);
+hipError_t launch_debug_exp(const double* x, int64_t n, double* out, hipStream_t st);
 
 }  // namespace clv

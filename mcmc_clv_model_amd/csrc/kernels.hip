@@ -13,14 +13,15 @@
 // replayed variates (CLV_RNG_REPLAY) trajectories agree with the reference to rounding.
 #include <hip/hip_ext.h>
 
+#include "fastmath.h"
 #include "kernels.h"
 #include "philox.h"
 
 namespace clv {
 
 
-__device__ __forceinline__ double clip70(double v) {  // np.clip(v, -70, 70), NaN passes (bi:323)
-  return v < -70.0 ? -70.0 : (v > 70.0 ? 70.0 : v);
+__device__ __forceinline__ double clip70(double v) {  // np.clip(v, -70, 70) for non-NaN v (bi:323)
+  return __builtin_fmin(__builtin_fmax(v, -70.0), 70.0);   // v_max_f64 + v_min_f64
 }
 __device__ __forceinline__ double min700(double v) {  // np.minimum(700, v) (bi:223)
   return v > 700.0 ? 700.0 : v;
@@ -40,23 +41,97 @@ __device__ __forceinline__ double log_post(const LPConst& c, double ll, double l
   return lm > 5.0 ? -__builtin_inf() : res;  // cap (quirk Q3)
 }
 
-// Deterministic workgroup reduction of NS doubles (fixed butterfly + fixed wave order).
+// Philox-mode log posterior up to a per-customer constant (only differences enter the MH test):
+// the quadratic prior of bi:303-306 expanded in (ll, lm) with per-customer linear coefficients,
+// the likelihood of bi:299-301, and ocml exp replaced by exp_fast (|ll|, |lm| <= 70 by the clip).
+//   lp = ll (A ll + B lm + Dl) + lm (C lm + El) - w (e^ll + e^lm)
+//   A = -p00/2, B = -p01, C = -p11/2, Dl = xm + p00 m0 + p01 m1, El = (1-z) + p01 m0 + p11 m1.
+// The lm > 5 cap (quirk Q3) is applied by the caller.
+struct LPFast {
+  double A, B, C, Dl, El, w;
+};
+__device__ __forceinline__ double log_post_fast(const LPFast& c, double ll, double lm, const double* tab) {
+  const double t1 = __builtin_fma(c.A, ll, __builtin_fma(c.B, lm, c.Dl));
+  const double t2 = __builtin_fma(c.C, lm, c.El);
+  const double q = __builtin_fma(ll, t1, lm * t2);
+  return __builtin_fma(-c.w, exp_fast(ll, tab) + exp_fast(lm, tab), q);
+}
+
+// ---- wave-level reduce-scatter on CDNA4 cross-lane instructions ----
+__device__ __forceinline__ uint64_t dbits(double x) { return __builtin_bit_cast(uint64_t, x); }
+__device__ __forceinline__ double bitsd(uint64_t x) { return __builtin_bit_cast(double, x); }
+
+// v_permlane32_swap: lanes 32-63 of a <-> lanes 0-31 of b (both dwords of each double).
+__device__ __forceinline__ void swap_halves(double& a, double& b) {
+  const uint64_t ua = dbits(a), ub = dbits(b);
+  const auto lo = __builtin_amdgcn_permlane32_swap((uint32_t)ua, (uint32_t)ub, false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap((uint32_t)(ua >> 32), (uint32_t)(ub >> 32), false, false);
+  a = bitsd(((uint64_t)hi[0] << 32) | lo[0]);
+  b = bitsd(((uint64_t)hi[1] << 32) | lo[1]);
+}
+// v_permlane16_swap: odd rows (16 lanes) of a <-> even rows of b.
+__device__ __forceinline__ void swap_rows(double& a, double& b) {
+  const uint64_t ua = dbits(a), ub = dbits(b);
+  const auto lo = __builtin_amdgcn_permlane16_swap((uint32_t)ua, (uint32_t)ub, false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap((uint32_t)(ua >> 32), (uint32_t)(ub >> 32), false, false);
+  a = bitsd(((uint64_t)hi[0] << 32) | lo[0]);
+  b = bitsd(((uint64_t)hi[1] << 32) | lo[1]);
+}
+// x + (x of the lane R places further round the 16-lane row), DPP row_ror:R (VALU, no LDS).
+template <int R>
+__device__ __forceinline__ double add_row_ror(double x) {
+  const uint64_t u = dbits(x);
+  const uint32_t lo = __builtin_amdgcn_update_dpp(0u, (uint32_t)u, 0x120 + R, 0xf, 0xf, false);
+  const uint32_t hi = __builtin_amdgcn_update_dpp(0u, (uint32_t)(u >> 32), 0x120 + R, 0xf, 0xf, false);
+  return x + bitsd(((uint64_t)hi << 32) | lo);
+}
+
+// Deterministic workgroup reduction of NS doubles.  Per wave: reduce-scatter across the halves
+// (v_permlane32_swap: element j stays in lanes 0-31, element j+H1 in lanes 32-63), then across
+// row pairs (v_permlane16_swap), then a 16-lane DPP rotate-allreduce of the remaining
+// ceil(NS/4) values — ~3 VALU per element-step, instead of 6 ds_bpermute butterflies of all NS
+// values.  Lane 0 of each row writes its row's values; waves are summed in fixed order.
 // Result valid in `out` (LDS) for all threads after the call.
 template <int NS>
 __device__ __forceinline__ void block_reduce(double (&v)[NS], double (*red)[NS], double* out) {
+  constexpr int H1 = (NS + 1) / 2;
+  constexpr int H2 = (H1 + 1) / 2;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   constexpr int NW = BLOCK / 64;
+  double w1[H1];
 #pragma unroll
-  for (int j = 0; j < NS; ++j) {
-    double t = v[j];
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) t += __shfl_xor(t, off, 64);
-    v[j] = t;
+  for (int j = 0; j < H1; ++j) {
+    double a = v[j];
+    double b = (j + H1 < NS) ? v[j + H1] : 0.0;
+    swap_halves(a, b);
+    w1[j] = a + b;  // lanes 0-31: element j;  lanes 32-63: element j + H1
   }
-  if (lane == 0) {
+  double w2[H2];
 #pragma unroll
-    for (int j = 0; j < NS; ++j) red[wave][j] = v[j];
+  for (int j = 0; j < H2; ++j) {
+    double a = w1[j];
+    double b = (j + H2 < H1) ? w1[j + H2] : 0.0;
+    swap_rows(a, b);
+    w2[j] = a + b;  // even rows: w1 index j;  odd rows: w1 index j + H2
+  }
+#pragma unroll
+  for (int j = 0; j < H2; ++j) {
+    double x = w2[j];
+    x = add_row_ror<8>(x);
+    x = add_row_ror<4>(x);
+    x = add_row_ror<2>(x);
+    x = add_row_ror<1>(x);
+    w2[j] = x;
+  }
+  if ((lane & 15) == 0) {
+    const int row = lane >> 4;
+#pragma unroll
+    for (int j = 0; j < H2; ++j) {
+      const int i1 = j + ((row & 1) ? H2 : 0);
+      const int idx = i1 + ((row >> 1) ? H1 : 0);
+      if (i1 < H1 && idx < NS) red[wave][idx] = w2[j];
+    }
   }
   __syncthreads();
   if (threadIdx.x < NS) {
@@ -405,6 +480,11 @@ __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
   constexpr int NS = NXY + NYY + 1;
   __shared__ double red[BLOCK / 64][NS];
   __shared__ double tot[NS];
+  __shared__ double exp_tab[64];
+  if constexpr (!REPLAY) {
+    load_exp_table(exp_tab);
+    __syncthreads();
+  }
 
   const Geometry& g = a.g;
   const int c = blockIdx.y;
@@ -534,8 +614,9 @@ __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
       const double s11 = H[H_S11];
       double ll = log(lam);
       double lm = log(mu);
-      double cur = log_post(lc, ll, lm);
+      double cur;
       if constexpr (REPLAY) {
+        cur = log_post(lc, ll, lm);
         for (int j = 0; j < g.S; ++j) {
           const double tl = tape[(int64_t)(2 + 3 * j) * g.n + i];
           const double tm = tape[(int64_t)(3 + 3 * j) * g.n + i];
@@ -556,11 +637,21 @@ __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
         constexpr int MC = MH_CHUNK_STEPS;
         float tl[MC], tm[MC], lu[MC];
         const SlotPhilox ph(k0, k1, gi, (uint32_t)s);
+        LPFast fc;
+        fc.A = -0.5 * lc.p00;
+        fc.B = -lc.p01;
+        fc.C = -0.5 * lc.p11;
+        fc.Dl = lc.xm + lc.p00 * lc.m0 + lc.p01 * lc.m1;
+        fc.El = lc.omz + lc.p01 * lc.m0 + lc.p11 * lc.m1;
+        fc.w = lc.w;
+        cur = lm > 5.0 ? -__builtin_inf() : log_post_fast(fc, ll, lm, exp_tab);
         auto step = [&](float t_l, float t_m, float l_u) {
-          const double pl = clip70(ll + s00 * (double)t_l);
-          const double pm = clip70(lm + s11 * (double)t_m);
-          const double plp = log_post(lc, pl, pm);
-          if ((plp - cur) > (double)l_u) {  // exp(d) > u  <=>  d > log(u)
+          const double pl = clip70(__builtin_fma(s00, (double)t_l, ll));
+          const double pm = clip70(__builtin_fma(s11, (double)t_m, lm));
+          const double plp = log_post_fast(fc, pl, pm, exp_tab);
+          // bi:329-335 with lp(proposal) = -inf for pm > 5 (Q3): accept iff pm <= 5 and
+          // exp(plp - cur) > u  <=>  plp - cur > log(u)  (cur = -inf accepts any finite proposal)
+          if (pm <= 5.0 && (plp - cur) > (double)l_u) {
             ll = pl;
             lm = pm;
             cur = plp;
@@ -780,6 +871,14 @@ __global__ void debug_hyper_variates_kernel(uint64_t seed, int chain, uint32_t s
   normals[i] = hyper_normal(k0, k1, HSLOT_NORMAL0, sweep + (uint32_t)i);
 }
 
+__global__ void debug_exp_kernel(const double* x, int64_t n, double* out) {
+  __shared__ double tab[64];
+  load_exp_table(tab);
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = exp_fast(x[i], tab);
+}
+
 // ---------------------------------------------------------------------------------------------
 // Dispatch
 // ---------------------------------------------------------------------------------------------
@@ -860,6 +959,11 @@ hipError_t launch_debug_hyper_variates(uint64_t seed, int chain, uint32_t sweep,
                                        double* chi2, double* normals, hipStream_t st) {
   hipLaunchKernelGGL(debug_hyper_variates_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, seed,
                      chain, sweep, df, n, chi2, normals);
+  return hipGetLastError();
+}
+
+hipError_t launch_debug_exp(const double* x, int64_t n, double* out, hipStream_t st) {
+  hipLaunchKernelGGL(debug_exp_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, n, out);
   return hipGetLastError();
 }
 

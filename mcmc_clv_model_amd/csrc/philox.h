@@ -17,6 +17,16 @@ namespace clv {
 
 struct u32x4 { uint32_t x, y, z, w; };
 
+// a ^ b ^ c in one VALU instruction on gfx950 (v_bitop3_b32, truth table 0x96); the compiler
+// emits two v_xor_b32 for the plain expression.
+CLV_HD uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+#else
+  return a ^ b ^ c;
+#endif
+}
+
 CLV_HD u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
@@ -24,7 +34,7 @@ CLV_HD u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
     const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
     const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
     const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
-    c = u32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    c = u32x4{xor3(hi1, c.y, k0), lo1, xor3(hi0, c.w, k1), lo0};
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;
   }
@@ -73,12 +83,12 @@ struct SlotPhilox {
   CLV_HD u32x4 operator()(uint32_t slot) const {
     // round 1 (key k)
     const uint64_t p1 = (uint64_t)0xCD9E8D57u * slot;
-    u32x4 c{(uint32_t)(p1 >> 32) ^ sweep ^ k0, (uint32_t)p1, r1z, r1w};
+    u32x4 c{xor3((uint32_t)(p1 >> 32), sweep, k0), (uint32_t)p1, r1z, r1w};
     uint32_t a0 = k0 + 0x9E3779B9u, a1 = k1 + 0xBB67AE85u;
     // round 2: the second product is slot-independent
     {
       const uint64_t q0 = (uint64_t)0xD2511F53u * c.x;
-      c = u32x4{(uint32_t)(p1r2 >> 32) ^ c.y ^ a0, (uint32_t)p1r2, (uint32_t)(q0 >> 32) ^ c.w ^ a1, (uint32_t)q0};
+      c = u32x4{xor3((uint32_t)(p1r2 >> 32), c.y, a0), (uint32_t)p1r2, xor3((uint32_t)(q0 >> 32), c.w, a1), (uint32_t)q0};
       a0 += 0x9E3779B9u;
       a1 += 0xBB67AE85u;
     }
@@ -86,7 +96,7 @@ struct SlotPhilox {
     for (int r = 2; r < 10; ++r) {
       const uint64_t q0 = (uint64_t)0xD2511F53u * c.x;
       const uint64_t q1 = (uint64_t)0xCD9E8D57u * c.z;
-      c = u32x4{(uint32_t)(q1 >> 32) ^ c.y ^ a0, (uint32_t)q1, (uint32_t)(q0 >> 32) ^ c.w ^ a1, (uint32_t)q0};
+      c = u32x4{xor3((uint32_t)(q1 >> 32), c.y, a0), (uint32_t)q1, xor3((uint32_t)(q0 >> 32), c.w, a1), (uint32_t)q0};
       a0 += 0x9E3779B9u;
       a1 += 0xBB67AE85u;
     }

@@ -11,6 +11,7 @@
 #define __builtin_amdgcn_cosf(x) (x)
 #define __builtin_amdgcn_sinf(x) (x)
 #define __builtin_amdgcn_rsqf(x) (x)
+#define __builtin_amdgcn_exp2f(x) (x)
 #include "../../mcmc_clv_model_amd/csrc/philox.h"
 
 int main() {

@@ -362,3 +362,18 @@ def test_sharded_sampler_rccl_matches_fused(L, graph_chunk):
     assert np.array_equal(bits(beta), bits(ref[2])) and np.array_equal(bits(sigma), bits(ref[3]))
     assert np.array_equal(bits(sums), bits(ref_sums))
     assert np.array_equal(bits(l2), bits(ref_l2)) and np.array_equal(bits(ll), bits(ref_ll))
+
+
+def test_device_fast_exp_accuracy(L):
+    """exp_fast (csrc/fastmath.h), used by the Philox-mode MH step on arguments clipped to
+    [-70, 70] (bi:323): <= 2 ulp from the correctly rounded exp (numpy's exp is within 1 ulp of
+    it, so the test allows 3 ulp against numpy) over the whole range and near 0."""
+    rng = np.random.default_rng(3)
+    x = np.concatenate([rng.uniform(-70, 70, 200_000), rng.uniform(-1e-3, 1e-3, 20_000),
+                        np.array([-70.0, 70.0, 0.0, -0.0, 1e-300, np.log(2) / 128, -np.log(2) / 128])])
+    out = np.zeros_like(x)
+    assert L.clv_debug_exp(_dp(x), x.size, _dp(out)) == 0
+    ref = np.exp(x)
+    ulp = np.abs(out - ref) / np.spacing(ref)
+    assert ulp.max() <= 3.0, ulp.max()
+    assert np.mean(out == ref) > 0.6
