@@ -106,6 +106,7 @@ def lib() -> ctypes.CDLL:
         "clv_debug_level2": (c_int32, [c_int32, c_int32, POINTER(ClvPrior), dp, dp, dp, dp, dp, dp, dp]),
         "clv_debug_hyper_variates": (c_int32, [c_uint64, c_int32, c_uint32, c_double, c_int64, dp, dp]),
         "clv_debug_stamps": (c_int32, [sp, POINTER(c_uint64)]),
+        "clv_debug_wg_stamps": (c_int32, [sp, POINTER(c_uint64)]),
         "clv_debug_exp": (c_int32, [dp, c_int64, dp]),
     }
     for name, (res, args) in sigs.items():

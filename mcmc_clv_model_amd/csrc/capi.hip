@@ -59,7 +59,7 @@ struct clv_sampler {
   double *d_block = nullptr, *d_unit = nullptr;
   double* d_prior = nullptr;
   Ctrl* d_ctrl = nullptr;
-  uint32_t* d_arrive = nullptr;     // [chain] fused-tail arrival counters
+  uint32_t* d_arrive = nullptr;     // fused-tail arrival counters: [chain], then [chain][units_per_rank]
   double* d_hvar = nullptr;         // [chain][HV] precomputed hyper variates
   unsigned long long* d_stamps = nullptr;  // CLV_STAMPS diagnostic build only
   double *d_level1 = nullptr, *d_level2 = nullptr, *d_loglik = nullptr, *d_sums = nullptr;
@@ -109,6 +109,8 @@ SweepArgs sweep_args(clv_sampler* s, int init, int fuse = 0) {
   a.init = init;
   a.fuse = fuse;
   a.chain_arrive = s->d_arrive;
+  a.unit_arrive = s->d_arrive + s->g.n_chains;
+  a.unitpart = s->d_unit;
   a.hvar_out = s->d_hvar;
   a.stamps = s->d_stamps;
   a.h = hyper_args(s, nullptr, 0);
@@ -357,18 +359,18 @@ int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* pri
   else s->d_unit = s->d_block;
   CLV_HIPC(dalloc(&s->d_prior, PRIOR_DOUBLES));
   CLV_HIPC(dalloc(&s->d_ctrl, 1));
-  CLV_HIPC(dalloc(&s->d_arrive, C));
+  CLV_HIPC(dalloc(&s->d_arrive, C + C * (int64_t)g.units_per_rank));  // chain, then unit counters
   CLV_HIPC(dalloc(&s->d_hvar, C * HV));
 #ifdef CLV_STAMPS
   {
-    std::vector<unsigned long long> st(1024 * 8, 0ull);
+    std::vector<unsigned long long> st(1024 * 8 + 4 * (size_t)C * std::max(nb_local, 1), 0ull);
     for (int i = 0; i < 1024; ++i) st[i * 8 + 0] = st[i * 8 + 4] = ~0ull;
     CLV_HIPC(dalloc(&s->d_stamps, st.size()));
     CLV_HIPC(hipMemcpy(s->d_stamps, st.data(), st.size() * sizeof(unsigned long long), hipMemcpyHostToDevice));
   }
 #endif
   CLV_HIPC(hipMemsetAsync(s->d_hvar, 0, sizeof(double) * C * HV, s->stream));
-  CLV_HIPC(hipMemsetAsync(s->d_arrive, 0, sizeof(uint32_t) * C, s->stream));
+  CLV_HIPC(hipMemsetAsync(s->d_arrive, 0, sizeof(uint32_t) * (C + C * (int64_t)g.units_per_rank), s->stream));
   CLV_HIPC(dalloc(&s->d_bs, C * (CLV_MAX_K * CLV_MAX_D + CLV_MAX_D * CLV_MAX_D)));
   if (g.n_draws > 0) {
     CLV_HIPC(dalloc(&s->d_level2, (size_t)C * g.n_draws * g.l2w));
@@ -704,6 +706,15 @@ int clv_debug_stamps(clv_sampler* s, uint64_t* out) {
   if (!s->d_stamps) return fail(CLV_ESTATE, "library not built with CLV_STAMPS (make STAMPS=1)");
   CLV_HIP(hipStreamSynchronize(s->stream));
   CLV_HIP(hipMemcpy(out, s->d_stamps, sizeof(uint64_t) * 1024 * 8, hipMemcpyDeviceToHost));
+  return CLV_OK;
+}
+
+int clv_debug_wg_stamps(clv_sampler* s, uint64_t* out) {
+  if (!s || !out) return fail(CLV_EINVAL, "null argument");
+  if (!s->d_stamps) return fail(CLV_ESTATE, "library not built with CLV_STAMPS (make STAMPS=1)");
+  CLV_HIP(hipStreamSynchronize(s->stream));
+  CLV_HIP(hipMemcpy(out, s->d_stamps + 1024 * 8, sizeof(uint64_t) * 4 * s->g.n_chains * s->g.nb_local,
+                    hipMemcpyDeviceToHost));
   return CLV_OK;
 }
 

@@ -91,6 +91,8 @@ struct SweepArgs {
   int init;                  // 1: initialisation pass (bi:367-370), no sweep
   int fuse;                  // 1: the chain's last-arriving workgroup performs the level-2 draw
   uint32_t* chain_arrive;    // [chain] arrival counters of the fused tail (zero between launches)
+  uint32_t* unit_arrive;     // [chain][units_per_rank] per-unit arrival counters (blocks_per_unit > 1)
+  double* unitpart;          // [chain][units_per_rank][stride] unit partials (blocks_per_unit > 1)
   double* hvar_out;          // [chain][HV]: the chain's last workgroup precomputes the next level-2
                              // draw's Philox variates at its start (off the critical path), or null
   HyperArgs h;               // level-2 arguments of the fused tail

@@ -156,7 +156,19 @@ __device__ __forceinline__ void stamp(unsigned long long* st, int64_t s, int k, 
   else __hip_atomic_fetch_max(p, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 #define CLV_STAMP(st, s, k, is_min) stamp(st, s, k, is_min)
+// per-workgroup record of the latest launch after the 1024 x 8 sweep stamps:
+// [start, end of customer work, HW_ID, XCC_ID] (placement diagnostics)
+__device__ __forceinline__ void wg_stamp(unsigned long long* st, int64_t wg, int k) {
+  if (!st) return;
+  unsigned long long v;
+  if (k < 2) v = __builtin_amdgcn_s_memrealtime();
+  else if (k == 2) v = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));   // HW_REG_HW_ID
+  else v = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11));             // HW_REG_XCC_ID
+  st[1024 * 8 + wg * 4 + k] = v;
+}
+#define CLV_WG_STAMP(st, wg, k) wg_stamp(st, wg, k)
 #else
+#define CLV_WG_STAMP(st, wg, k) ((void)0)
 #define CLV_STAMP(st, s, k, is_min) ((void)0)
 #endif
 
@@ -371,10 +383,11 @@ __device__ double chi2_draw(uint32_t k0, uint32_t k1, uint32_t sweep, int idx, d
 // fixed-order sum of all unit partials, variates, algebra, hyper state, level-2 record and
 // log-likelihood, then the sweep-counter arrival.  Executed by one 256-thread workgroup: the
 // standalone hyper_kernel (sharded path) or the last-arriving sweep workgroup of the chain
-// (fused path).  `blocks` != nullptr: read block partials and form each unit's sum on the fly
-// with the exact order of group_kernel (so both paths are bitwise identical).
+// (fused path).  `units`: [world][chain][units_per_rank][stride] unit partials (the gathered
+// buffer; at world size 1 this rank's unit partials, or its block partials when a unit is one
+// block), summed in global unit order — so every path and GPU count is bitwise identical.
 template <int D, int K, bool REPLAY, int NS>
-__device__ void hyper_body(const HyperArgs& a, int c, int64_t s, int mode, const double* blocks,
+__device__ void hyper_body(const HyperArgs& a, int c, int64_t s, int mode, const double* units,
                            double (*red)[NS], double* tot, double* var_iw, double* var_chi, double* var_noise) {
   constexpr int NTRIL = D * (D - 1) / 2;
   const Geometry& g = a.g;
@@ -404,27 +417,17 @@ __device__ void hyper_body(const HyperArgs& a, int c, int64_t s, int mode, const
       var_chi[q] = chi2_draw(k0, k1, (uint32_t)hs, q, a.nu_n - D + 1 + q);
     }
   }
-  // 2. fixed-order reduction over all units of all shards (independent of world size)
+  // 2. fixed-order reduction over all units of all shards (independent of world size).  Unit
+  // partials are read with sc1 loads: in the fused path other CUs wrote them during this launch.
   double acc[NS];
 #pragma unroll
   for (int j = 0; j < NS; ++j) acc[j] = 0.0;
   for (int64_t u = tid; u < g.n_units_global; u += 256) {
-    if (blocks) {  // world_size == 1: units formed from this chain's block partials
-      const double* p = blocks + ((int64_t)c * g.blocks_per_rank + u * g.blocks_per_unit) * g.stride;
+    const int64_t r = u / g.units_per_rank;
+    const int64_t lu = u - r * g.units_per_rank;
+    const double* p = units + ((r * g.n_chains + c) * g.units_per_rank + lu) * g.stride;
 #pragma unroll
-      for (int j = 0; j < NS; ++j) {
-        double t = 0.0;
-        for (int bb = 0; bb < g.blocks_per_unit; ++bb)
-          t += __hip_atomic_load(p + (int64_t)bb * g.stride + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        acc[j] += t;
-      }
-    } else {
-      const int64_t r = u / g.units_per_rank;
-      const int64_t lu = u - r * g.units_per_rank;
-      const double* p = a.units + ((r * g.n_chains + c) * g.units_per_rank + lu) * g.stride;
-#pragma unroll
-      for (int j = 0; j < NS; ++j) acc[j] += p[j];
-    }
+    for (int j = 0; j < NS; ++j) acc[j] += __hip_atomic_load(p + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   block_reduce<NS>(acc, red, tot);  // its barriers also publish the variates written to LDS above
 
@@ -467,7 +470,7 @@ __global__ __launch_bounds__(256) void hyper_kernel(HyperArgs a) {
   __shared__ double var_iw[4], var_chi[4], var_noise[32];
   const int64_t done = __hip_atomic_load(&a.ctrl->cur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int64_t s = a.mode == 1 ? 0 : done + 1;  // sweep whose statistics are reduced here
-  hyper_body<D, K, REPLAY, NS>(a, blockIdx.x, s, a.mode, nullptr, red, tot, var_iw, var_chi, var_noise);
+  hyper_body<D, K, REPLAY, NS>(a, blockIdx.x, s, a.mode, a.units, red, tot, var_iw, var_chi, var_noise);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -500,6 +503,9 @@ __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
   if (threadIdx.x == 0 && !a.init) {
     CLV_STAMP(a.stamps, s, 0, true);
     CLV_STAMP(a.stamps, s, 5, false);
+    CLV_WG_STAMP(a.stamps, (int64_t)c * g.nb_local + b, 0);
+    CLV_WG_STAMP(a.stamps, (int64_t)c * g.nb_local + b, 2);
+    CLV_WG_STAMP(a.stamps, (int64_t)c * g.nb_local + b, 3);
   }
 
   // ---- the next level-2 draw's Philox variates (independent of the statistics): computed by
@@ -753,21 +759,52 @@ __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
     __hip_atomic_store(a.blockpart + ((int64_t)c * g.blocks_per_rank + b) * g.stride + threadIdx.x, tot[threadIdx.x],
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
-  // ---- fused level-2 draw (world_size == 1): the chain's last workgroup to arrive reduces all
-  // block partials and draws (beta, Sigma) — no separate hyper launch per sweep.  Hand-off in the
-  // fence-free form of the MI355X guide (Guideline 16 / "Valid forms"): partials and variates are
-  // stored sc1 (write-through), every wave drains its stores, one lane takes an agent-scope
-  // ticket; the last arriver reads every handed-off value with sc1 loads (no L1 hit possible).
+  // ---- fused level-2 draw (world_size == 1): no separate hyper launch per sweep.  Two-level
+  // hand-off: the last-arriving workgroup of each unit (blocks_per_unit consecutive blocks) sums
+  // the unit's block partials in group_kernel's order; the last unit of the chain to complete
+  // reduces all unit partials and draws (beta, Sigma).  Hand-off in the fence-free form of the
+  // MI355X guide (Guideline 16 / "Valid forms"): partials and variates are stored sc1
+  // (write-through), every wave drains its stores, one lane takes an agent-scope ticket; the
+  // last arriver reads every handed-off value with sc1 loads (no L1 hit possible).
   if (a.fuse) {
     __shared__ uint32_t s_last;
     __shared__ double var_iw[4], var_chi[4], var_noise[32];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    const int bpu = g.blocks_per_unit;
+    const double* units = a.blockpart;  // a unit is one block
+    if (bpu > 1) {
+      const int u = b / bpu;
+      const int nbu = min(bpu, g.nb_local - u * bpu);  // blocks of this unit in the launch
+      if (threadIdx.x == 0) {
+        uint32_t* ctr = a.unit_arrive + (int64_t)c * g.units_per_rank + u;
+        const uint32_t old = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t last = old == (uint32_t)(nbu - 1) ? 1u : 0u;
+        if (last) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = last;
+      }
+      __syncthreads();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only
+      if (!s_last) return;
+      if (threadIdx.x < NS) {  // unit partial: sequential over the unit's blocks (= group_kernel)
+        const double* p = a.blockpart + ((int64_t)c * g.blocks_per_rank + (int64_t)u * bpu) * g.stride + threadIdx.x;
+        double t = 0.0;
+        for (int bb = 0; bb < bpu; ++bb)
+          t += __hip_atomic_load(p + (int64_t)bb * g.stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(a.unitpart + ((int64_t)c * g.units_per_rank + u) * g.stride + threadIdx.x, t,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      units = a.unitpart;
+    }
     if (threadIdx.x == 0) {
       CLV_STAMP(a.stamps, s, 1, false);
       CLV_STAMP(a.stamps, s, 4, true);
+      CLV_WG_STAMP(a.stamps, (int64_t)c * g.nb_local + b, 1);
+      const uint32_t n_arrivals = (uint32_t)((g.nb_local + bpu - 1) / bpu);  // units in the launch
       const uint32_t old = __hip_atomic_fetch_add(a.chain_arrive + c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint32_t last = old == (uint32_t)(g.nb_local - 1) ? 1u : 0u;
+      const uint32_t last = old == n_arrivals - 1 ? 1u : 0u;
       if (last) __hip_atomic_store(a.chain_arrive + c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       s_last = last;
     }
@@ -775,7 +812,7 @@ __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only
     if (s_last) {
       if (threadIdx.x == 0) CLV_STAMP(a.stamps, s, 2, false);
-      hyper_body<D, K, REPLAY, NS>(a.h, c, s, 0, a.blockpart, red, tot, var_iw, var_chi, var_noise);
+      hyper_body<D, K, REPLAY, NS>(a.h, c, s, 0, units, red, tot, var_iw, var_chi, var_noise);
       if (threadIdx.x == 0) CLV_STAMP(a.stamps, s, 3, false);
     }
   }

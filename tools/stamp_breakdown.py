@@ -40,6 +40,23 @@ def main(workload="c2", sweeps=1500, chains=None):
     print(f"  last block start:                       {us(rel[:, 5]):8.2f} us")
     print(f"  last block end -> tail start:           {us(st[:, 2] - st[:, 1]):8.2f} us")
     print(f"  tail (level-2 draw):                    {us(st[:, 3] - st[:, 2]):8.2f} us")
+    # placement of the latest launch's workgroups: per CU (XCC, SE, CU) count and durations
+    nb = -(-s.n // 256)
+    wg = np.zeros(s.chains * nb * 4, np.uint64)
+    assert s._L.clv_debug_wg_stamps(s.h, wg.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))) == 0
+    wg = wg.reshape(-1, 4).astype(np.int64)
+    hw, xcc = wg[:, 2], wg[:, 3] & 0xF
+    cu, se = (hw >> 8) & 0xF, (hw >> 13) & 0x7
+    key = xcc * 1000 + se * 100 + cu
+    uniq, cnt = np.unique(key, return_counts=True)
+    dur = (wg[:, 1] - wg[:, 0]) * 0.01
+    per_wg_cnt = cnt[np.searchsorted(uniq, key)]
+    print(f"  workgroups {len(wg)} on {len(uniq)} CUs; WGs per CU histogram:",
+          {int(k): int(v) for k, v in zip(*np.unique(cnt, return_counts=True))})
+    for k in sorted(set(per_wg_cnt.tolist())):
+        d = dur[per_wg_cnt == k]
+        print(f"    CUs with {k} WG(s): WG customer-phase duration median {np.median(d):7.2f} us, max {d.max():7.2f} us")
+    print("  WGs per XCC:", {int(k): int(v) for k, v in zip(*np.unique(xcc, return_counts=True))})
     s.close()
 
 
