@@ -125,8 +125,8 @@ int clv_run(clv_sampler* s, int64_t n_sweeps);
  *   after clv_create, bivariate only: [exchange] clv_hyper   (initial draw, bi:393 of sweep 1)
  *   per sweep:                        clv_sweep, [exchange] clv_hyper
  * (bivariate: the hyper after sweep s is bi:393 of sweep s+1; trivariate: tri:529 of sweep s).
- * clv_partials() exposes this shard's unit partials, [chain][units_per_rank][stride] doubles;
- * clv_hyper() reads the gathered buffer [world][chain][units_per_rank][stride]
+ * clv_partials() exposes this shard's unit partials, [chain][stride][units_per_rank] doubles;
+ * clv_hyper() reads the gathered buffer [world][chain][stride][units_per_rank]
  * (NULL = the local buffer, world_size == 1) and sums it in global unit order. */
 int clv_sweep(clv_sampler* s);
 int clv_hyper(clv_sampler* s, const double* gathered_device_ptr);

@@ -138,6 +138,7 @@ HyperArgs hyper_args(clv_sampler* s, const double* units, int mode) {
   a.nu_n = s->prior.nu_n;
   a.omega2 = s->prior.omega2;
   a.mode = mode;
+  a.stamps = s->d_stamps;
   // mode 0 follows a sweep kernel, which precomputed the draw's variates (if it had workgroups)
   a.hvar = (mode == 0 && !s->replay && s->g.nb_local > 0) ? s->d_hvar : nullptr;
   return a;

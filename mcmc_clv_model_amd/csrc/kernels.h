@@ -56,7 +56,7 @@ struct Rng {
 struct HyperArgs {
   Geometry g;
   Rng r;
-  const double* units;       // [world][chain][units_per_rank][stride]
+  const double* units;       // [world][chain][stride][units_per_rank] (statistic-major: coalesced reads)
   double* hyper;             // [chain][HS]
   Ctrl* ctrl;
   double* level2;            // [chain][n_draws][l2w]
@@ -69,6 +69,7 @@ struct HyperArgs {
   double omega2;
   int mode;                  // 0: after sweep (cur+1); 1: bivariate initial draw (sweep 1)
   const double* hvar;        // [chain][HV] Philox variates precomputed by the sweep kernel, or null
+  unsigned long long* stamps; // diagnostic build only (CLV_STAMPS)
 };
 
 struct SweepArgs {
@@ -82,7 +83,7 @@ struct SweepArgs {
   double* lam;               // [chain][n]
   double* mu;
   const double* hyper;       // [chain][HS]
-  double* blockpart;         // [chain][blocks_per_rank][stride]
+  double* blockpart;         // [chain][stride][blocks_per_rank]
   const Ctrl* ctrl;
   double* level1;            // [chain][n_draws][n][D+2] or null
   double* sums;              // [chain][CLV_N_SUM_STATS][n] or null
@@ -92,7 +93,7 @@ struct SweepArgs {
   int fuse;                  // 1: the chain's last-arriving workgroup performs the level-2 draw
   uint32_t* chain_arrive;    // [chain] arrival counters of the fused tail (zero between launches)
   uint32_t* unit_arrive;     // [chain][units_per_rank] per-unit arrival counters (blocks_per_unit > 1)
-  double* unitpart;          // [chain][units_per_rank][stride] unit partials (blocks_per_unit > 1)
+  double* unitpart;          // [chain][stride][units_per_rank] unit partials (blocks_per_unit > 1)
   double* hvar_out;          // [chain][HV]: the chain's last workgroup precomputes the next level-2
                              // draw's Philox variates at its start (off the critical path), or null
   HyperArgs h;               // level-2 arguments of the fused tail
@@ -102,7 +103,7 @@ struct SweepArgs {
 struct GroupArgs {
   Geometry g;
   const double* blockpart;
-  double* unitpart;          // [chain][units_per_rank][stride]
+  double* unitpart;          // [chain][stride][units_per_rank]
 };
 
 

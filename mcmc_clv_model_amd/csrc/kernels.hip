@@ -92,13 +92,13 @@ __device__ __forceinline__ double add_row_ror(double x) {
 // ceil(NS/4) values — ~3 VALU per element-step, instead of 6 ds_bpermute butterflies of all NS
 // values.  Lane 0 of each row writes its row's values; waves are summed in fixed order.
 // Result valid in `out` (LDS) for all threads after the call.
-template <int NS>
+template <int NS, int NT = BLOCK>
 __device__ __forceinline__ void block_reduce(double (&v)[NS], double (*red)[NS], double* out) {
   constexpr int H1 = (NS + 1) / 2;
   constexpr int H2 = (H1 + 1) / 2;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  constexpr int NW = BLOCK / 64;
+  constexpr int NW = NT / 64;
   double w1[H1];
 #pragma unroll
   for (int j = 0; j < H1; ++j) {
@@ -188,10 +188,10 @@ __global__ __launch_bounds__(64) void group_kernel(GroupArgs a) {
   const int c = blockIdx.y;
   const int j = threadIdx.x;
   if (j >= g.stride) return;
-  const double* p = a.blockpart + ((int64_t)c * g.blocks_per_rank + (int64_t)u * g.blocks_per_unit) * g.stride + j;
+  const double* p = a.blockpart + ((int64_t)c * g.stride + j) * g.blocks_per_rank + (int64_t)u * g.blocks_per_unit;
   double t = 0.0;
-  for (int bb = 0; bb < g.blocks_per_unit; ++bb) t += p[(int64_t)bb * g.stride];
-  a.unitpart[((int64_t)c * g.units_per_rank + u) * g.stride + j] = t;
+  for (int bb = 0; bb < g.blocks_per_unit; ++bb) t += p[bb];
+  a.unitpart[((int64_t)c * g.stride + j) * g.units_per_rank + u] = t;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -221,11 +221,9 @@ __device__ void cholesky(const double (&A)[D][D], double (&L)[D][D]) {
 
 // hyper-state finalisation from (beta, Sigma): inverse block, proposal scales, eta constants.
 template <int D, int K>
-__device__ void finalize_hyper(const double (&beta)[K][D], const double (&Sig)[D][D], double omega2, double* H) {
+__device__ void finalize_hyper(const double* beta_flat, const double (&Sig)[D][D], double omega2, double* H) {
 #pragma unroll
-  for (int k = 0; k < K; ++k)
-#pragma unroll
-    for (int d = 0; d < D; ++d) H[H_BETA + k * D + d] = beta[k][d];
+  for (int q = 0; q < K * D; ++q) H[H_BETA + q] = beta_flat[q];
   for (int q = 0; q < 9; ++q) H[H_SIGMA + q] = 0.0;
 #pragma unroll
   for (int p = 0; p < D; ++p)
@@ -255,104 +253,145 @@ __device__ void finalize_hyper(const double (&beta)[K][D], const double (&Sig)[D
   H[H_S11] = Sig[1][1];
 }
 
-// Given the reduced statistics and the variates, draw (beta, Sigma).
-// iwn: n_tril normals, chi2: D chi-square draws, noise: either the replayed mvn noise (w, D*K) or
-// standard normals z (D*K) mapped through kron(chol(Sigma), chol(V)).
+// LDS scratch of the level-2 draw.
+struct L2Scratch {
+  double prior[81 + 81 + 27 + 9];  // V, chol(V), A0 B0, S0 + B0'A0B0 (staged at the tail's start)
+  double R[CLV_MAX_K * 3];   // X'Y + A0 B0            [k*D + d]
+  double Bh[CLV_MAX_K * 3];  // B_hat = V R            [k*D + d]
+  double Sn[6];              // S_n upper triangle     (p, q >= p) order
+  double Sig[9];             // Sigma                  [p*D + q]
+  double Ls[9];              // chol(Sigma)            [p*D + q]
+  double beta[CLV_MAX_K * 3];// beta = B_hat + w       [k*D + d] (= beta.ravel() row-major)
+};
+
+// Orders LDS accesses between the lanes of one wavefront (LDS operations of a wave complete in
+// order; the fences keep the compiler from moving accesses across).
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Stage the prior block (V, chol V, A0 B0, S0B: 198 doubles) into the scratch; a later barrier
+// publishes it.
+__device__ __forceinline__ void stage_prior(const double* prior, L2Scratch* sc) {
+  for (int t = threadIdx.x; t < 198; t += blockDim.x) sc->prior[t] = prior[t];
+}
+
+// Given the reduced statistics `tot` (LDS), the variates (LDS) and the staged prior, draw
+// (beta, Sigma) with wavefront 0 (lanes >= 64 return at once; no workgroup barriers).  Element-parallel phases
+// (one lane per element of B_hat, S_n, w) around a one-lane D x D core; each element's sum runs in
+// the sequential order of bi:243-261, so the result does not depend on the lane mapping.
+// iwn: n_tril normals, chi2: D chi-square draws, noise: either the replayed mvn noise (w, D*K)
+// or standard normals z (D*K) mapped through kron(chol(Sigma), chol(V)).
 template <int D, int K>
-__device__ void level2_draw(const double* tot, const double* V, const double* cholV, const double* A0B0,
-                            const double* S0B, const double* iwn, const double* chi2, const double* noise,
-                            bool noise_is_w, double (&beta)[K][D], double (&Sig)[D][D]) {
+__device__ void level2_draw(const double* tot, const double* iwn, const double* chi2, const double* noise,
+                            bool noise_is_w, L2Scratch* sc) {
   constexpr int NXY = K * D;
-  double R[K][D], Bh[K][D];
+  const int t = threadIdx.x;
+  if (t >= 64) return;
+  const double* V = sc->prior;
+  const double* cholV = sc->prior + 81;
+  const double* A0B0 = sc->prior + 162;
+  const double* S0B = sc->prior + 189;
+  if (t < NXY) sc->R[t] = tot[t] + A0B0[t];
+  wave_sync();
+  if (t < NXY) {  // B_hat[k][d] = sum_j V[k][j] R[j][d]
+    const int k = t / D, d = t % D;
+    double sv = 0.0;
 #pragma unroll
-  for (int k = 0; k < K; ++k)
-#pragma unroll
-    for (int d = 0; d < D; ++d) R[k][d] = tot[k * D + d] + A0B0[k * D + d];
-#pragma unroll
-  for (int k = 0; k < K; ++k)
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-      double sv = 0.0;
-#pragma unroll
-      for (int j = 0; j < K; ++j) sv += V[k * K + j] * R[j][d];
-      Bh[k][d] = sv;
-    }
-  // S_n = S0 + Y'Y + B0'A0B0 - R'B_hat   (== S0 + E'E + C'A0C, bi:253-255)
-  double Sn[D][D];
-  int t = NXY;
-#pragma unroll
-  for (int p = 0; p < D; ++p)
-#pragma unroll
-    for (int q = p; q < D; ++q) {
-      double rb = 0.0;
-#pragma unroll
-      for (int k = 0; k < K; ++k) rb += R[k][p] * Bh[k][q];
-      const double v = (S0B[p * D + q] + tot[t++]) - rb;
-      Sn[p][q] = v;
-      Sn[q][p] = v;
-    }
-  // Sigma ~ IW(nu_n, S_n): scipy invwishart Bartlett form, Sigma = (L A^-1)(L A^-1)'
-  double L[D][D], A[D][D], M[D][D];
-  cholesky<D>(Sn, L);
-#pragma unroll
-  for (int p = 0; p < D; ++p)
-#pragma unroll
-    for (int q = 0; q < D; ++q) A[p][q] = 0.0;
-  {
-    int n = 0;
-#pragma unroll
-    for (int p = 1; p < D; ++p)
-#pragma unroll
-      for (int q = 0; q < p; ++q) A[p][q] = iwn[n++];  // np.tril_indices(D, -1) order
-#pragma unroll
-    for (int p = 0; p < D; ++p) A[p][p] = sqrt(chi2[p]);
+    for (int j = 0; j < K; ++j) sv += V[k * K + j] * sc->R[j * D + d];
+    sc->Bh[t] = sv;
   }
-#pragma unroll
-  for (int r = 0; r < D; ++r)
-#pragma unroll
-    for (int j = D - 1; j >= 0; --j) {
-      double sv = L[r][j];
-#pragma unroll
-      for (int k = j + 1; k < D; ++k) sv -= M[r][k] * A[k][j];
-      M[r][j] = sv / A[j][j];
+  wave_sync();
+  if (t < D * (D + 1) / 2) {  // S_n = S0 + Y'Y + B0'A0B0 - R'B_hat   (== S0 + E'E + C'A0C, bi:253-255)
+    int p = 0, q = t;
+    while (q >= D - p) {
+      q -= D - p;
+      ++p;
     }
+    q += p;
+    double rb = 0.0;
 #pragma unroll
-  for (int p = 0; p < D; ++p)
-#pragma unroll
-    for (int q = 0; q < D; ++q) {
-      double sv = 0.0;
-#pragma unroll
-      for (int k = 0; k < D; ++k) sv += M[p][k] * M[q][k];
-      Sig[p][q] = sv;
-    }
-#pragma unroll
-  for (int p = 0; p < D; ++p)
-#pragma unroll
-    for (int q = p + 1; q < D; ++q) Sig[q][p] = Sig[p][q];
-  // beta | Sigma: MVN(B_hat.ravel(), kron(Sigma, V)) with the reference's row-major ravel (quirk Q1)
-  double w[D * K];
-  if (noise_is_w) {
-#pragma unroll
-    for (int q = 0; q < D * K; ++q) w[q] = noise[q];
-  } else {
-    double Ls[D][D];
-    cholesky<D>(Sig, Ls);
+    for (int k = 0; k < K; ++k) rb += sc->R[k * D + p] * sc->Bh[k * D + q];
+    sc->Sn[t] = (S0B[p * D + q] + tot[NXY + t]) - rb;
+  }
+  wave_sync();
+  if (t == 0) {
+    double Sn[D][D];
+    int n = 0;
 #pragma unroll
     for (int p = 0; p < D; ++p)
 #pragma unroll
-      for (int bq = 0; bq < K; ++bq) {
+      for (int q = p; q < D; ++q) {
+        Sn[p][q] = sc->Sn[n];
+        Sn[q][p] = sc->Sn[n++];
+      }
+    // Sigma ~ IW(nu_n, S_n): scipy invwishart Bartlett form, Sigma = (L A^-1)(L A^-1)'
+    double L[D][D], A[D][D], M[D][D], Sig[D][D];
+    cholesky<D>(Sn, L);
+#pragma unroll
+    for (int p = 0; p < D; ++p)
+#pragma unroll
+      for (int q = 0; q < D; ++q) A[p][q] = 0.0;
+    {
+      int m = 0;
+#pragma unroll
+      for (int p = 1; p < D; ++p)
+#pragma unroll
+        for (int q = 0; q < p; ++q) A[p][q] = iwn[m++];  // np.tril_indices(D, -1) order
+#pragma unroll
+      for (int p = 0; p < D; ++p) A[p][p] = sqrt(chi2[p]);
+    }
+#pragma unroll
+    for (int r = 0; r < D; ++r)
+#pragma unroll
+      for (int j = D - 1; j >= 0; --j) {
+        double sv = L[r][j];
+#pragma unroll
+        for (int k = j + 1; k < D; ++k) sv -= M[r][k] * A[k][j];
+        M[r][j] = sv / A[j][j];
+      }
+#pragma unroll
+    for (int p = 0; p < D; ++p)
+#pragma unroll
+      for (int q = 0; q < D; ++q) {
         double sv = 0.0;
 #pragma unroll
-        for (int cc = 0; cc <= p; ++cc)
+        for (int k = 0; k < D; ++k) sv += M[p][k] * M[q][k];
+        Sig[p][q] = sv;
+      }
 #pragma unroll
-          for (int e = 0; e <= bq; ++e) sv += Ls[p][cc] * cholV[bq * K + e] * noise[cc * K + e];
-        w[p * K + bq] = sv;
+    for (int p = 0; p < D; ++p)
+#pragma unroll
+      for (int q = p + 1; q < D; ++q) Sig[q][p] = Sig[p][q];
+    double Ls[D][D];
+    if (!noise_is_w) cholesky<D>(Sig, Ls);
+#pragma unroll
+    for (int p = 0; p < D; ++p)
+#pragma unroll
+      for (int q = 0; q < D; ++q) {
+        sc->Sig[p * D + q] = Sig[p][q];
+        sc->Ls[p * D + q] = noise_is_w ? 0.0 : Ls[p][q];
       }
   }
-#pragma unroll
-  for (int k = 0; k < K; ++k)
-#pragma unroll
-    for (int d = 0; d < D; ++d) beta[k][d] = Bh[k][d] + w[k * D + d];
+  wave_sync();
+  // beta | Sigma: MVN(B_hat.ravel(), kron(Sigma, V)) with the reference's row-major ravel (quirk
+  // Q1): flat element q = p*K + bq of the noise pairs with beta.ravel()[q] = beta[q / D][q % D]
+  if (t < NXY) {
+    double w;
+    if (noise_is_w) {
+      w = noise[t];
+    } else {
+      const int p = t / K, bq = t % K;
+      double sv = 0.0;
+      for (int cc = 0; cc <= p; ++cc)
+        for (int e = 0; e <= bq; ++e) sv += sc->Ls[p * D + cc] * cholV[bq * K + e] * noise[cc * K + e];
+      w = sv;
+    }
+    sc->beta[t] = sc->Bh[t] + w;
+  }
+  wave_sync();
 }
 
 // Philox-mode hyper variates (fp64).
@@ -383,17 +422,19 @@ __device__ double chi2_draw(uint32_t k0, uint32_t k1, uint32_t sweep, int idx, d
 // fixed-order sum of all unit partials, variates, algebra, hyper state, level-2 record and
 // log-likelihood, then the sweep-counter arrival.  Executed by one 256-thread workgroup: the
 // standalone hyper_kernel (sharded path) or the last-arriving sweep workgroup of the chain
-// (fused path).  `units`: [world][chain][units_per_rank][stride] unit partials (the gathered
+// (fused path).  `units`: [world][chain][stride][units_per_rank] unit partials (the gathered
 // buffer; at world size 1 this rank's unit partials, or its block partials when a unit is one
 // block), summed in global unit order — so every path and GPU count is bitwise identical.
-template <int D, int K, bool REPLAY, int NS>
+template <int D, int K, bool REPLAY, int NS, int NT>
 __device__ void hyper_body(const HyperArgs& a, int c, int64_t s, int mode, const double* units,
-                           double (*red)[NS], double* tot, double* var_iw, double* var_chi, double* var_noise) {
+                           double (*red)[NS], double* tot, double* var_iw, double* var_chi, double* var_noise,
+                           L2Scratch* l2) {
   constexpr int NTRIL = D * (D - 1) / 2;
   const Geometry& g = a.g;
   const int tid = threadIdx.x;
   const int64_t hs = (D == 2) ? s + 1 : s;  // sweep the drawn (beta, Sigma) belongs to
 
+  stage_prior(a.V, l2);  // published by block_reduce's barriers
   // 1. variates first: independent of the statistics, so their loads overlap the reduction's
   if constexpr (REPLAY) {
     const double* tv = a.r.tape + ((int64_t)c * a.r.tape_sweeps + (hs - 1)) * a.r.tape_sweep_stride +
@@ -410,10 +451,10 @@ __device__ void hyper_body(const HyperArgs& a, int c, int64_t s, int mode, const
     uint32_t k0, k1;
     chain_key(a.r.seed, (int64_t)a.r.chain_first + c, &k0, &k1);
     if (tid < NTRIL) var_iw[tid] = hyper_normal(k0, k1, HSLOT_NORMAL0 + tid, (uint32_t)hs);
-    if (tid >= 64 && tid < 64 + D * K)
-      var_noise[tid - 64] = hyper_normal(k0, k1, HSLOT_BETA_NORMAL0 + (tid - 64), (uint32_t)hs);
-    if (tid >= 128 && tid < 128 + D) {
-      const int q = tid - 128;
+    if (tid >= 32 && tid < 32 + D * K)
+      var_noise[tid - 32] = hyper_normal(k0, k1, HSLOT_BETA_NORMAL0 + (tid - 32), (uint32_t)hs);
+    if (tid >= 64 && tid < 64 + D) {  // second wavefront: the gamma rejection loops
+      const int q = tid - 64;
       var_chi[q] = chi2_draw(k0, k1, (uint32_t)hs, q, a.nu_n - D + 1 + q);
     }
   }
@@ -422,27 +463,33 @@ __device__ void hyper_body(const HyperArgs& a, int c, int64_t s, int mode, const
   double acc[NS];
 #pragma unroll
   for (int j = 0; j < NS; ++j) acc[j] = 0.0;
-  for (int64_t u = tid; u < g.n_units_global; u += 256) {
+  for (int64_t u = tid; u < g.n_units_global; u += NT) {
     const int64_t r = u / g.units_per_rank;
     const int64_t lu = u - r * g.units_per_rank;
-    const double* p = units + ((r * g.n_chains + c) * g.units_per_rank + lu) * g.stride;
+    const double* p = units + (r * g.n_chains + c) * g.stride * (int64_t)g.units_per_rank + lu;
 #pragma unroll
-    for (int j = 0; j < NS; ++j) acc[j] += __hip_atomic_load(p + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int j = 0; j < NS; ++j)  // lanes read consecutive units: coalesced
+      acc[j] += __hip_atomic_load(p + (int64_t)j * g.units_per_rank, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  block_reduce<NS>(acc, red, tot);  // its barriers also publish the variates written to LDS above
+  block_reduce<NS, NT>(acc, red, tot);  // its barriers also publish the variates written to LDS above
 
-  // 3. algebra + outputs (one lane)
+  // 3. algebra (element-parallel phases + one-lane core) and outputs
+  if (tid == 0) CLV_STAMP(a.stamps, s, 6, false);
+  L2Scratch* sc = l2;
+  level2_draw<D, K>(tot, var_iw, var_chi, var_noise, REPLAY, sc);
+  const bool store_l2 = hs >= 1 && is_stored(hs, g);
+  double* o = store_l2 ? a.level2 + ((int64_t)c * g.n_draws + draw_index(hs, g)) * g.l2w : nullptr;
+  if (tid < K * D && store_l2) o[(tid % D) * K + tid / D] = sc->beta[tid];  // beta.T.ravel() (bi:411)
   if (tid == 0) {
-    double beta[K][D], Sig[D][D];
-    level2_draw<D, K>(tot, a.V, a.cholV, a.A0B0, a.S0B, var_iw, var_chi, var_noise, REPLAY, beta, Sig);
-    finalize_hyper<D, K>(beta, Sig, a.omega2, a.hyper + (int64_t)c * HS);
-    if (hs >= 1 && is_stored(hs, g)) {
-      double* o = a.level2 + ((int64_t)c * g.n_draws + draw_index(hs, g)) * g.l2w;
-      int q = 0;
+    double Sig[D][D];
 #pragma unroll
-      for (int d = 0; d < D; ++d)
+    for (int p = 0; p < D; ++p)
 #pragma unroll
-        for (int k = 0; k < K; ++k) o[q++] = beta[k][d];  // beta.T.ravel() (bi:411)
+      for (int q = 0; q < D; ++q) Sig[p][q] = sc->Sig[p * D + q];
+    finalize_hyper<D, K>(sc->beta, Sig, a.omega2, a.hyper + (int64_t)c * HS);
+    CLV_STAMP(a.stamps, s, 7, false);
+    if (store_l2) {
+      int q = K * D;
 #pragma unroll
       for (int p = 0; p < D; ++p)
 #pragma unroll
@@ -453,7 +500,9 @@ __device__ void hyper_body(const HyperArgs& a, int c, int64_t s, int mode, const
     if (mode == 0) {
       // the last chain to finish advances the sweep counter (every workgroup of this launch has
       // read it before arriving)
-      const uint32_t old = __hip_atomic_fetch_add(&a.ctrl->arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      // relaxed: the next launch reads cur and the hyper state after the kernel boundary (whose
+      // release/acquire makes them visible); an acq_rel RMW here would write back the whole L2
+      const uint32_t old = __hip_atomic_fetch_add(&a.ctrl->arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (old == (uint32_t)g.n_chains - 1) {
         __hip_atomic_store(&a.ctrl->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&a.ctrl->cur, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -468,16 +517,224 @@ __global__ __launch_bounds__(256) void hyper_kernel(HyperArgs a) {
   __shared__ double red[4][NS];
   __shared__ double tot[NS];
   __shared__ double var_iw[4], var_chi[4], var_noise[32];
+  __shared__ L2Scratch l2;
   const int64_t done = __hip_atomic_load(&a.ctrl->cur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int64_t s = a.mode == 1 ? 0 : done + 1;  // sweep whose statistics are reduced here
-  hyper_body<D, K, REPLAY, NS>(a, blockIdx.x, s, a.mode, a.units, red, tot, var_iw, var_chi, var_noise);
+  hyper_body<D, K, REPLAY, NS, 256>(a, blockIdx.x, s, a.mode, a.units, red, tot, var_iw, var_chi, var_noise, &l2);
 }
 
 // ---------------------------------------------------------------------------------------------
 // Sweep kernel
 // ---------------------------------------------------------------------------------------------
+// One customer's sweep state (per lane and task).
+template <int D, int K>
+struct Cust {
+  int64_t i;          // local customer index (clamped to a valid row for inactive tasks)
+  bool active;
+  double xr[K];       // [1, covariates]
+  double tx, T, xm;
+  double lam, mu, eta, tau;
+  bool z;
+  double ll, lm, cur; // MH state (log scale) and its log posterior
+  LPFast fc;          // Philox-mode log-posterior coefficients
+  LPConst lc;         // replay-mode log-posterior constants
+  uint32_t gi;        // global customer index (Philox counter)
+};
+
+// Phase A (bi:193-227, bi:280-290): load, draw_z, draw_tau, log-posterior constants.
+template <int D, int K, bool REPLAY>
+__device__ __forceinline__ void cust_prepare(Cust<D, K>& u, const SweepArgs& a, int c, int64_t s, const double* H,
+                                             uint32_t k0, uint32_t k1, const double* tape, const double* exp_tab) {
+  const Geometry& g = a.g;
+  const int64_t i = u.i;
+  u.tx = a.tx[i];
+  u.T = a.T[i];
+  u.xr[0] = 1.0;
+#pragma unroll
+  for (int k = 1; k < K; ++k) u.xr[k] = a.cov[(int64_t)(k - 1) * g.n + i];
+  const int64_t ci = (int64_t)c * g.n + i;
+  const double lam = a.lam[ci];
+  const double mu = a.mu[ci];
+  u.lam = lam;
+  u.mu = mu;
+  u.xm = (double)a.x[i];
+  u.gi = (uint32_t)(g.shard_begin + i);
+  const double tx = u.tx, T = u.T;
+
+  // ---- draw_z (bi:193-200)
+  // Replay: u_z and the per-customer tau variate (standard exponential if alive, uniform if
+  // churned — the reference's consumption order, bi:215-225). Philox: slot SLOT_ZTAU words
+  // (x, y) -> u_z, (z, w) -> U in [0,1) for churned / -log(U') with U' in (0,1] for alive.
+  double u_z;
+  uint32_t rz = 0, rw = 0;
+  double v_tau = 0.0;
+  if constexpr (REPLAY) {
+    u_z = tape[i];
+    v_tau = tape[g.n + i];
+  } else {
+    const u32x4 r = customer_block(k0, k1, u.gi, (uint32_t)s, SLOT_ZTAU);
+    u_z = u53(r.x, r.y);
+    rz = r.z;
+    rw = r.w;
+  }
+  const double ml = mu + lam;
+  const double zz = ml * (T - tx);
+  const double e = exp(-zz);
+  const double p = (ml * e) / (ml * e + mu * (1.0 - e));
+  const bool z = u_z < p;
+  u.z = z;
+
+  // ---- draw_tau (bi:203-227)
+  double tau;
+  if (z) {
+    double E;
+    if constexpr (REPLAY) E = v_tau; else E = -log(u53_open0(rz, rw));
+    tau = T + (1.0 / mu) * E;
+  } else {
+    double uu;
+    if constexpr (REPLAY) uu = v_tau; else uu = u53(rz, rw);
+    const double ml_tx = min700(ml * tx);
+    const double ml_T = min700(ml * T);
+    tau = -log((1 - uu) * exp(-ml_tx) + uu * exp(-ml_T)) / ml;
+  }
+  u.tau = tau;
+
+  // ---- _draw_level_1 (bi:268-339): mv_mean = X @ beta (bi:284)
+  double m0 = 0.0, m1 = 0.0;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    m0 += u.xr[k] * H[H_BETA + k * D + 0];
+    m1 += u.xr[k] * H[H_BETA + k * D + 1];
+  }
+  LPConst& lc = u.lc;
+  lc.xm = u.xm;
+  lc.omz = z ? 0.0 : 1.0;
+  lc.w = z ? T : tau;
+  lc.m0 = m0;
+  lc.m1 = m1;
+  lc.p00 = H[H_P00];
+  lc.p01 = H[H_P01];
+  lc.p11 = H[H_P11];
+  u.ll = log(lam);
+  u.lm = log(mu);
+  if constexpr (REPLAY) {
+    u.cur = log_post(lc, u.ll, u.lm);
+  } else {
+    LPFast& fc = u.fc;
+    fc.A = -0.5 * lc.p00;
+    fc.B = -lc.p01;
+    fc.C = -0.5 * lc.p11;
+    fc.Dl = lc.xm + lc.p00 * lc.m0 + lc.p01 * lc.m1;
+    fc.El = lc.omz + lc.p01 * lc.m0 + lc.p11 * lc.m1;
+    fc.w = lc.w;
+    u.cur = u.lm > 5.0 ? -__builtin_inf() : log_post_fast(fc, u.ll, u.lm, exp_tab);
+  }
+}
+
+// One Philox-mode MH step (bi:316-335) with lp(proposal) = -inf for pm > 5 (Q3): accept iff
+// pm <= 5 and exp(plp - cur) > u  <=>  plp - cur > log(u)  (cur = -inf accepts any finite one).
+template <int D, int K>
+__device__ __forceinline__ void mh_step(Cust<D, K>& u, double s00, double s11, float t_l, float t_m, float l_u,
+                                        const double* exp_tab) {
+  const double pl = clip70(__builtin_fma(s00, (double)t_l, u.ll));
+  const double pm = clip70(__builtin_fma(s11, (double)t_m, u.lm));
+  const double plp = log_post_fast(u.fc, pl, pm, exp_tab);
+  if (pm <= 5.0 && (plp - u.cur) > (double)l_u) {
+    u.ll = pl;
+    u.lm = pm;
+    u.cur = plp;
+  }
+}
+
+// Phase C: state update (bi:337-338), draw_eta (tri:306-333), storage (bi:402-428, tri:539-571),
+// the customer's sufficient statistics into acc.
+template <int D, int K, bool REPLAY, int NS>
+__device__ __forceinline__ void cust_finish(Cust<D, K>& u, const SweepArgs& a, int c, int64_t s, bool stored,
+                                            const double* H, uint32_t k0, uint32_t k1, const double* tape,
+                                            double (&acc)[NS]) {
+  constexpr int NXY = K * D;
+  const Geometry& g = a.g;
+  const int64_t i = u.i;
+  double lam = exp(u.ll);  // bi:337-338
+  double mu = exp(u.lm);
+  double eta = 1.0, Y[D];
+  const bool z = u.z;
+  if constexpr (D == 3) {
+    double m2 = 0.0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) m2 += u.xr[k] * H[H_BETA + k * D + 2];
+    const double post_var = H[H_POSTVAR];
+    const double post_mean = post_var * (a.log_s[i] / H[H_OMEGA2] + m2 / H[H_S22]);
+    double zeta;
+    if constexpr (REPLAY) {
+      zeta = tape[(int64_t)(2 + 3 * g.S) * g.n + i];
+    } else {
+      const u32x4 r = customer_block(k0, k1, u.gi, (uint32_t)s, SLOT_ETA);
+      zeta = sqrt(-2.0 * log(u53_open0(r.x, r.y))) * cospi(2.0 * u53(r.z, r.w));
+    }
+    eta = exp(post_mean + H[H_SQRT_POSTVAR] * zeta);
+    // tri: level 2 sees log(lambda) before the storage round trip (tri:529-536 before :542)
+    Y[0] = log(lam);
+    Y[1] = log(mu);
+    Y[2] = log(eta);
+  }
+  double lik = 0.0;
+  if (stored) {
+    lam = exp(log(lam));  // quirk Q5 (bi:405-406)
+    mu = exp(log(mu));
+    const int64_t dr = draw_index(s, g);
+    if (a.level1) {
+      double* o = a.level1 + (((int64_t)c * g.n_draws + dr) * g.n + i) * (D + 2);
+      o[0] = lam;
+      o[1] = mu;
+      o[2] = u.tau;
+      o[3] = z ? 1.0 : 0.0;
+      if constexpr (D == 3) o[4] = eta;
+    }
+    const double lgl = log(lam), lgm = log(mu);
+    lik = (u.xm * lgl + u.lc.omz * lgm) - (lam + mu) * u.lc.w;  // bi:423-427
+    if (a.sums) {
+      double* sm = a.sums + (int64_t)c * CLV_N_SUM_STATS * g.n + i;
+      sm[CLV_SUM_LAMBDA * g.n] += lam;
+      sm[CLV_SUM_MU * g.n] += mu;
+      sm[CLV_SUM_Z * g.n] += z ? 1.0 : 0.0;
+      sm[CLV_SUM_LOG_LAMBDA * g.n] += lgl;
+      sm[CLV_SUM_LOG_MU * g.n] += lgm;
+      sm[CLV_SUM_LAMBDA2 * g.n] += lam * lam;
+      sm[CLV_SUM_MU2 * g.n] += mu * mu;
+      if constexpr (D == 3) {
+        sm[CLV_SUM_ETA * g.n] += eta;
+        sm[CLV_SUM_LOG_ETA * g.n] += log(eta);
+      }
+    }
+  }
+  if constexpr (D == 2) {
+    // bi: the next level-2 draw uses log of the carried state (bi:393)
+    Y[0] = log(lam);
+    Y[1] = log(mu);
+  }
+  const int64_t ci = (int64_t)c * g.n + i;
+  a.lam[ci] = lam;
+  a.mu[ci] = mu;
+  // ---- sufficient statistics: X'Y (K x D), Y'Y (upper triangle), likelihood term
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+#pragma unroll
+    for (int d = 0; d < D; ++d) acc[k * D + d] += u.xr[k] * Y[d];
+  int t = NXY;
+#pragma unroll
+  for (int p = 0; p < D; ++p)
+#pragma unroll
+    for (int q = p; q < D; ++q) acc[t++] += Y[p] * Y[q];
+  acc[NS - 1] += lik;
+}
+
+// One workgroup = one statistics block of BLOCK customers of one chain, one customer per lane.
+// (Two interleaved customers per lane for ILP at CDNOW size measured slower — 35 vs 23 us/sweep —
+// and would tie the statistics' summation order to the lane mapping.)
 template <int D, int K, bool REPLAY>
 __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
+  constexpr int NT = BLOCK;
   constexpr int NXY = K * D;
   constexpr int NYY = D * (D + 1) / 2;
   constexpr int NS = NXY + NYY + 1;
@@ -492,8 +749,6 @@ __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
   const Geometry& g = a.g;
   const int c = blockIdx.y;
   const int b = blockIdx.x;
-  const int64_t i = (int64_t)b * BLOCK + threadIdx.x;
-  const bool active = i < g.n;
   const int64_t s = a.init ? 0 : __hip_atomic_load(&a.ctrl->cur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
   const bool stored = !a.init && is_stored(s, g);
 
@@ -509,10 +764,10 @@ __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
   }
 
   // ---- the next level-2 draw's Philox variates (independent of the statistics): computed by
-  // wave 3 of the chain's last workgroup — the partially filled one — so the draw's serial
-  // tail only loads them.  Written with sc1 (write-through) stores.
+  // the last wavefront of the chain's last workgroup — the partially filled one — so the draw's
+  // serial tail only loads them.  Written with sc1 (write-through) stores.
   if constexpr (!REPLAY) {
-    if (a.hvar_out && !a.init && b == g.nb_local - 1 && (threadIdx.x >> 6) == 3) {
+    if (a.hvar_out && !a.init && b == g.nb_local - 1 && (int)(threadIdx.x >> 6) == NT / 64 - 1) {
       const int l = threadIdx.x & 63;
       const int64_t hs = (D == 2) ? s + 1 : s;
       uint32_t k0, k1;
@@ -533,230 +788,98 @@ __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
     }
   }
 
-  if (active) {
-    const double* H = a.hyper + (int64_t)c * HS;
-    const int64_t ci = (int64_t)c * g.n + i;
-    const double tx = a.tx[i];
-    const double T = a.T[i];
-    double xr[K];
-    xr[0] = 1.0;
-#pragma unroll
-    for (int k = 1; k < K; ++k) xr[k] = a.cov[(int64_t)(k - 1) * g.n + i];
+  Cust<D, K> cu;
+  {
+    const int64_t i = (int64_t)b * BLOCK + threadIdx.x;
+    cu.active = i < g.n;
+    cu.i = cu.active ? i : (g.n > 0 ? g.n - 1 : 0);
+  }
 
-    double lam, mu, eta = 1.0, Y[D];
-    if (a.init) {
-      // bi:368-370 / tri:489-491
-      lam = a.lam_init;
-      mu = 1.0 / (tx + 0.5 / a.lam_init);
+  if (a.init) {
+    // bi:368-370 / tri:489-491: initial state and the statistics of the first level-2 draw
+    if (cu.active) {
+      const int64_t i = cu.i;
+      const double tx = a.tx[i];
+      const double lam = a.lam_init;
+      const double mu = 1.0 / (tx + 0.5 / a.lam_init);
+      double xr[K], Y[D];
+      xr[0] = 1.0;
+#pragma unroll
+      for (int k = 1; k < K; ++k) xr[k] = a.cov[(int64_t)(k - 1) * g.n + i];
       Y[0] = log(lam);
       Y[1] = log(mu);
       if constexpr (D == 3) Y[2] = 0.0;
+      const int64_t ci = (int64_t)c * g.n + i;
+      a.lam[ci] = lam;
+      a.mu[ci] = mu;
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+#pragma unroll
+        for (int d = 0; d < D; ++d) acc[k * D + d] += xr[k] * Y[d];
+      int t = NXY;
+#pragma unroll
+      for (int p = 0; p < D; ++p)
+#pragma unroll
+        for (int r = p; r < D; ++r) acc[t++] += Y[p] * Y[r];
+    }
+  } else if (cu.active) {
+    const double* H = a.hyper + (int64_t)c * HS;
+    uint32_t k0 = 0, k1 = 0;
+    const double* tape = nullptr;
+    if constexpr (REPLAY) {
+      tape = a.r.tape + ((int64_t)c * a.r.tape_sweeps + (s - 1)) * a.r.tape_sweep_stride;
     } else {
-      lam = a.lam[ci];
-      mu = a.mu[ci];
-      const double xm = (double)a.x[i];
-      uint32_t k0 = 0, k1 = 0;
-      const double* tape = nullptr;
-      if constexpr (REPLAY) {
-        tape = a.r.tape + ((int64_t)c * a.r.tape_sweeps + (s - 1)) * a.r.tape_sweep_stride;
-      } else {
-        chain_key(a.r.seed, (int64_t)a.r.chain_first + c, &k0, &k1);
-      }
-      const uint32_t gi = (uint32_t)(g.shard_begin + i);
-
-      // ---- draw_z (bi:193-200)
-      // Replay: u_z and the per-customer tau variate (standard exponential if alive, uniform if
-      // churned — the reference's consumption order, bi:215-225). Philox: slot SLOT_ZTAU words
-      // (x, y) -> u_z, (z, w) -> U in [0,1) for churned / -log(U') with U' in (0,1] for alive.
-      double u_z;
-      uint32_t rz = 0, rw = 0;
-      double v_tau = 0.0;
-      if constexpr (REPLAY) {
-        u_z = tape[i];
-        v_tau = tape[g.n + i];
-      } else {
-        const u32x4 r = customer_block(k0, k1, gi, (uint32_t)s, SLOT_ZTAU);
-        u_z = u53(r.x, r.y);
-        rz = r.z;
-        rw = r.w;
-      }
-      const double ml = mu + lam;
-      const double zz = ml * (T - tx);
-      const double e = exp(-zz);
-      const double p = (ml * e) / (ml * e + mu * (1.0 - e));
-      const bool z = u_z < p;
-
-      // ---- draw_tau (bi:203-227)
-      double tau;
-      if (z) {
-        double E;
-        if constexpr (REPLAY) E = v_tau; else E = -log(u53_open0(rz, rw));
-        tau = T + (1.0 / mu) * E;
-      } else {
-        double u;
-        if constexpr (REPLAY) u = v_tau; else u = u53(rz, rw);
-        const double ml_tx = min700(ml * tx);
-        const double ml_T = min700(ml * T);
-        tau = -log((1 - u) * exp(-ml_tx) + u * exp(-ml_T)) / ml;
-      }
-
-      // ---- _draw_level_1 (bi:268-339): mv_mean = X @ beta (bi:284)
-      double m0 = 0.0, m1 = 0.0;
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        m0 += xr[k] * H[H_BETA + k * D + 0];
-        m1 += xr[k] * H[H_BETA + k * D + 1];
-      }
-      LPConst lc;
-      lc.xm = xm;
-      lc.omz = z ? 0.0 : 1.0;
-      lc.w = z ? T : tau;
-      lc.m0 = m0;
-      lc.m1 = m1;
-      lc.p00 = H[H_P00];
-      lc.p01 = H[H_P01];
-      lc.p11 = H[H_P11];
-      const double s00 = H[H_S00];
-      const double s11 = H[H_S11];
-      double ll = log(lam);
-      double lm = log(mu);
-      double cur;
-      if constexpr (REPLAY) {
-        cur = log_post(lc, ll, lm);
+      chain_key(a.r.seed, (int64_t)a.r.chain_first + c, &k0, &k1);
+    }
+    cust_prepare<D, K, REPLAY>(cu, a, c, s, H, k0, k1, tape, exp_tab);
+    const double s00 = H[H_S00];
+    const double s11 = H[H_S11];
+    if constexpr (REPLAY) {
+      {
+        Cust<D, K>& u = cu;
         for (int j = 0; j < g.S; ++j) {
-          const double tl = tape[(int64_t)(2 + 3 * j) * g.n + i];
-          const double tm = tape[(int64_t)(3 + 3 * j) * g.n + i];
-          const double u = tape[(int64_t)(4 + 3 * j) * g.n + i];
-          const double pl = clip70(ll + s00 * tl);
-          const double pm = clip70(lm + s11 * tm);
-          const double plp = log_post(lc, pl, pm);
-          if (exp(plp - cur) > u) {  // bi:329-335
-            ll = pl;
-            lm = pm;
-            cur = plp;
-          }
-        }
-      } else {
-        // Software pipeline: the Philox blocks and t3 transforms of the next chunk of 4 MH steps
-        // are independent of the state, so they are generated while the current chunk's fp64
-        // accept/reject chain runs (ILP for the ~1.5 waves/SIMD of the CDNOW-sized problem).
-        constexpr int MC = MH_CHUNK_STEPS;
-        float tl[MC], tm[MC], lu[MC];
-        const SlotPhilox ph(k0, k1, gi, (uint32_t)s);
-        LPFast fc;
-        fc.A = -0.5 * lc.p00;
-        fc.B = -lc.p01;
-        fc.C = -0.5 * lc.p11;
-        fc.Dl = lc.xm + lc.p00 * lc.m0 + lc.p01 * lc.m1;
-        fc.El = lc.omz + lc.p01 * lc.m0 + lc.p11 * lc.m1;
-        fc.w = lc.w;
-        cur = lm > 5.0 ? -__builtin_inf() : log_post_fast(fc, ll, lm, exp_tab);
-        auto step = [&](float t_l, float t_m, float l_u) {
-          const double pl = clip70(__builtin_fma(s00, (double)t_l, ll));
-          const double pm = clip70(__builtin_fma(s11, (double)t_m, lm));
-          const double plp = log_post_fast(fc, pl, pm, exp_tab);
-          // bi:329-335 with lp(proposal) = -inf for pm > 5 (Q3): accept iff pm <= 5 and
-          // exp(plp - cur) > u  <=>  plp - cur > log(u)  (cur = -inf accepts any finite proposal)
-          if (pm <= 5.0 && (plp - cur) > (double)l_u) {
-            ll = pl;
-            lm = pm;
-            cur = plp;
-          }
-        };
-        const int n_chunks = (g.S + MC - 1) / MC;
-        if (n_chunks > 0) mh_chunk_variates(ph, 0u, tl, tm, lu);
-        for (int q = 0; q < n_chunks; ++q) {
-          float ntl[MC], ntm[MC], nlu[MC];
-          if (q + 1 < n_chunks) mh_chunk_variates(ph, (uint32_t)(q + 1), ntl, ntm, nlu);
-#pragma unroll
-          for (int i = 0; i < MC; ++i)
-            if (q * MC + i < g.S) step(tl[i], tm[i], lu[i]);  // uniform guard: last chunk may be partial
-#pragma unroll
-          for (int i = 0; i < MC; ++i) {
-            tl[i] = ntl[i];
-            tm[i] = ntm[i];
-            lu[i] = nlu[i];
+          const double tl = tape[(int64_t)(2 + 3 * j) * g.n + u.i];
+          const double tm = tape[(int64_t)(3 + 3 * j) * g.n + u.i];
+          const double uu = tape[(int64_t)(4 + 3 * j) * g.n + u.i];
+          const double pl = clip70(u.ll + s00 * tl);
+          const double pm = clip70(u.lm + s11 * tm);
+          const double plp = log_post(u.lc, pl, pm);
+          if (exp(plp - u.cur) > uu) {  // bi:329-335
+            u.ll = pl;
+            u.lm = pm;
+            u.cur = plp;
           }
         }
       }
-      lam = exp(ll);  // bi:337-338
-      mu = exp(lm);
-
-      // ---- draw_eta (tri:306-333, call site tri:524-526)
-      if constexpr (D == 3) {
-        double m2 = 0.0;
+    } else {
+      // Software pipeline: the Philox blocks and t3 transforms of the next chunk of 4 MH steps
+      // are independent of the state, so they are generated while the current chunk's fp64
+      // accept/reject chain runs (ILP for the ~1.5 waves/SIMD of the CDNOW-sized problem).
+      constexpr int MC = MH_CHUNK_STEPS;
+      float tl[MC], tm[MC], lu[MC];
+      const SlotPhilox ph(k0, k1, cu.gi, (uint32_t)s);
+      const int n_chunks = (g.S + MC - 1) / MC;
+      if (n_chunks > 0) mh_chunk_variates(ph, 0u, tl, tm, lu);
+      for (int ch = 0; ch < n_chunks; ++ch) {
+        float ntl[MC], ntm[MC], nlu[MC];
+        if (ch + 1 < n_chunks) mh_chunk_variates(ph, (uint32_t)(ch + 1), ntl, ntm, nlu);
 #pragma unroll
-        for (int k = 0; k < K; ++k) m2 += xr[k] * H[H_BETA + k * D + 2];
-        const double post_var = H[H_POSTVAR];
-        const double post_mean = post_var * (a.log_s[i] / H[H_OMEGA2] + m2 / H[H_S22]);
-        double zeta;
-        if constexpr (REPLAY) {
-          zeta = tape[(int64_t)(2 + 3 * g.S) * g.n + i];
-        } else {
-          const u32x4 r = customer_block(k0, k1, gi, (uint32_t)s, SLOT_ETA);
-          zeta = sqrt(-2.0 * log(u53_open0(r.x, r.y))) * cospi(2.0 * u53(r.z, r.w));
+        for (int st = 0; st < MC; ++st)
+          if (ch * MC + st < g.S) mh_step(cu, s00, s11, tl[st], tm[st], lu[st], exp_tab);  // last chunk may be partial
+#pragma unroll
+        for (int st = 0; st < MC; ++st) {
+          tl[st] = ntl[st];
+          tm[st] = ntm[st];
+          lu[st] = nlu[st];
         }
-        eta = exp(post_mean + H[H_SQRT_POSTVAR] * zeta);
-        // tri: level 2 sees log(lambda) before the storage round trip (tri:529-536 before :542)
-        Y[0] = log(lam);
-        Y[1] = log(mu);
-        Y[2] = log(eta);
-      }
-
-      // ---- storage (bi:402-428, tri:539-571)
-      if (stored) {
-        lam = exp(log(lam));  // quirk Q5 (bi:405-406)
-        mu = exp(log(mu));
-        const int64_t dr = draw_index(s, g);
-        if (a.level1) {
-          double* o = a.level1 + (((int64_t)c * g.n_draws + dr) * g.n + i) * (D + 2);
-          o[0] = lam;
-          o[1] = mu;
-          o[2] = tau;
-          o[3] = z ? 1.0 : 0.0;
-          if constexpr (D == 3) o[4] = eta;
-        }
-        const double lgl = log(lam), lgm = log(mu);
-        acc[NS - 1] = (xm * lgl + lc.omz * lgm) - (lam + mu) * lc.w;  // bi:423-427
-        if (a.sums) {
-          double* sm = a.sums + (int64_t)c * CLV_N_SUM_STATS * g.n + i;
-          sm[CLV_SUM_LAMBDA * g.n] += lam;
-          sm[CLV_SUM_MU * g.n] += mu;
-          sm[CLV_SUM_Z * g.n] += z ? 1.0 : 0.0;
-          sm[CLV_SUM_LOG_LAMBDA * g.n] += lgl;
-          sm[CLV_SUM_LOG_MU * g.n] += lgm;
-          sm[CLV_SUM_LAMBDA2 * g.n] += lam * lam;
-          sm[CLV_SUM_MU2 * g.n] += mu * mu;
-          if constexpr (D == 3) {
-            sm[CLV_SUM_ETA * g.n] += eta;
-            sm[CLV_SUM_LOG_ETA * g.n] += log(eta);
-          }
-        }
-      }
-      if constexpr (D == 2) {
-        // bi: the next level-2 draw uses log of the carried state (bi:393)
-        Y[0] = log(lam);
-        Y[1] = log(mu);
       }
     }
-    a.lam[ci] = lam;
-    a.mu[ci] = mu;
-
-    // ---- sufficient statistics: X'Y (K x D) and Y'Y (upper triangle)
-#pragma unroll
-    for (int k = 0; k < K; ++k)
-#pragma unroll
-      for (int d = 0; d < D; ++d) acc[k * D + d] = xr[k] * Y[d];
-    int t = NXY;
-#pragma unroll
-    for (int p = 0; p < D; ++p)
-#pragma unroll
-      for (int q = p; q < D; ++q) acc[t++] = Y[p] * Y[q];
+    cust_finish<D, K, REPLAY, NS>(cu, a, c, s, stored, H, k0, k1, tape, acc);
   }
 
   block_reduce<NS>(acc, red, tot);
   if (threadIdx.x < NS)  // sc1 (write-through) store: read cross-CU by the fused tail
-    __hip_atomic_store(a.blockpart + ((int64_t)c * g.blocks_per_rank + b) * g.stride + threadIdx.x, tot[threadIdx.x],
+    __hip_atomic_store(a.blockpart + ((int64_t)c * g.stride + threadIdx.x) * g.blocks_per_rank + b, tot[threadIdx.x],
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
   // ---- fused level-2 draw (world_size == 1): no separate hyper launch per sweep.  Two-level
@@ -769,6 +892,7 @@ __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
   if (a.fuse) {
     __shared__ uint32_t s_last;
     __shared__ double var_iw[4], var_chi[4], var_noise[32];
+    __shared__ L2Scratch l2;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     const int bpu = g.blocks_per_unit;
@@ -787,11 +911,18 @@ __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only
       if (!s_last) return;
       if (threadIdx.x < NS) {  // unit partial: sequential over the unit's blocks (= group_kernel)
-        const double* p = a.blockpart + ((int64_t)c * g.blocks_per_rank + (int64_t)u * bpu) * g.stride + threadIdx.x;
+        const double* p = a.blockpart + ((int64_t)c * g.stride + threadIdx.x) * g.blocks_per_rank + (int64_t)u * bpu;
         double t = 0.0;
-        for (int bb = 0; bb < bpu; ++bb)
-          t += __hip_atomic_load(p + (int64_t)bb * g.stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(a.unitpart + ((int64_t)c * g.units_per_rank + u) * g.stride + threadIdx.x, t,
+        int bb = 0;
+        for (; bb + 8 <= bpu; bb += 8) {  // batch the sc1 loads, add in order
+          double v[8];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) v[q] = __hip_atomic_load(p + bb + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) t += v[q];
+        }
+        for (; bb < bpu; ++bb) t += __hip_atomic_load(p + bb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(a.unitpart + ((int64_t)c * g.stride + threadIdx.x) * g.units_per_rank + u, t,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -812,7 +943,7 @@ __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only
     if (s_last) {
       if (threadIdx.x == 0) CLV_STAMP(a.stamps, s, 2, false);
-      hyper_body<D, K, REPLAY, NS>(a.h, c, s, 0, units, red, tot, var_iw, var_chi, var_noise);
+      hyper_body<D, K, REPLAY, NS, NT>(a.h, c, s, 0, units, red, tot, var_iw, var_chi, var_noise, &l2);
       if (threadIdx.x == 0) CLV_STAMP(a.stamps, s, 3, false);
     }
   }
@@ -824,12 +955,10 @@ __global__ void set_hyper_kernel(int n_chains, double* hyper, const double* bs, 
   const int c = threadIdx.x;
   if (c >= n_chains) return;
   const double* in = bs + (int64_t)c * (K * D + D * D);
-  double beta[K][D], Sig[D][D];
-  for (int k = 0; k < K; ++k)
-    for (int d = 0; d < D; ++d) beta[k][d] = in[k * D + d];
+  double Sig[D][D];
   for (int p = 0; p < D; ++p)
     for (int q = 0; q < D; ++q) Sig[p][q] = in[K * D + p * D + q];
-  finalize_hyper<D, K>(beta, Sig, omega2, hyper + (int64_t)c * HS);
+  finalize_hyper<D, K>(in, Sig, omega2, hyper + (int64_t)c * HS);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -876,26 +1005,26 @@ __global__ void debug_variates_kernel(uint64_t seed, int chain, uint32_t sweep, 
 // in: [V 81][cholV 81][A0B0 27][S0B 9] prior block, then xty(K*D) yty(D*D) iwn(3) chi2(3) z(D*K)
 template <int D, int K>
 __global__ void debug_level2_kernel(const double* prior, const double* in, double* out) {
-  if (threadIdx.x != 0) return;
-  const double* V = prior;
-  const double* cholV = prior + 81;
-  const double* A0B0 = prior + 162;
-  const double* S0B = prior + 189;
   constexpr int NXY = K * D;
-  double tot[NXY + D * (D + 1) / 2 + 1];
-  for (int q = 0; q < NXY; ++q) tot[q] = in[q];
-  int t = NXY;
-  for (int p = 0; p < D; ++p)
-    for (int q = p; q < D; ++q) tot[t++] = in[NXY + p * D + q];
+  __shared__ double tot[NXY + D * (D + 1) / 2 + 1];
+  __shared__ L2Scratch sc;
+  if (threadIdx.x == 0) {
+    for (int q = 0; q < NXY; ++q) tot[q] = in[q];
+    int t = NXY;
+    for (int p = 0; p < D; ++p)
+      for (int q = p; q < D; ++q) tot[t++] = in[NXY + p * D + q];
+  }
+  __syncthreads();
   const double* iwn = in + NXY + D * D;
   const double* chi = iwn + 3;
   const double* z = chi + 3;
-  double beta[K][D], Sig[D][D];
-  level2_draw<D, K>(tot, V, cholV, A0B0, S0B, iwn, chi, z, false, beta, Sig);
-  for (int k = 0; k < K; ++k)
-    for (int d = 0; d < D; ++d) out[k * D + d] = beta[k][d];
-  for (int p = 0; p < D; ++p)
-    for (int q = 0; q < D; ++q) out[K * D + p * D + q] = Sig[p][q];
+  stage_prior(prior, &sc);
+  __syncthreads();
+  level2_draw<D, K>(tot, iwn, chi, z, false, &sc);
+  if (threadIdx.x == 0) {
+    for (int q = 0; q < K * D; ++q) out[q] = sc.beta[q];
+    for (int q = 0; q < D * D; ++q) out[K * D + q] = sc.Sig[q];
+  }
 }
 
 __global__ void debug_hyper_variates_kernel(uint64_t seed, int chain, uint32_t sweep, double df, int64_t n,
@@ -985,7 +1114,7 @@ hipError_t launch_debug_variates(uint64_t seed, int chain, uint32_t sweep, int64
 hipError_t launch_debug_level2(int D, int K, const double* prior_dev, const double* in, double* out,
                                hipStream_t st) {
 #define CLV_CASE(DD, KK, RR) \
-  if (D == DD && K == KK) { hipLaunchKernelGGL((debug_level2_kernel<DD, KK>), dim3(1), dim3(64), 0, st, prior_dev, in, out); return hipGetLastError(); }
+  if (D == DD && K == KK) { hipLaunchKernelGGL((debug_level2_kernel<DD, KK>), dim3(1), dim3(256), 0, st, prior_dev, in, out); return hipGetLastError(); }
   CLV_FOR_K(CLV_CASE, 2, 0)
   CLV_FOR_K(CLV_CASE, 3, 0)
 #undef CLV_CASE

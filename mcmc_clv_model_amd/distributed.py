@@ -5,7 +5,7 @@ each rank sweeps its own contiguous customer range; the only coupling is the lev
 (bivariate/mcmc.py:233-262), which needs the sufficient statistics X'Y, Y'Y of ALL customers.
 Per sweep each rank publishes its unit partials, one ``all_gather_into_tensor`` over
 torch.distributed (backend "nccl" = RCCL over xGMI on MI355X; "gloo" in the CPU tests)
-assembles [world][chain][units_per_rank][stride], and every rank performs the identical
+assembles [world][chain][stride][units_per_rank], and every rank performs the identical
 fixed-order sum and the identical level-2 draw (same Philox counter), so no broadcast is needed
 and results are bitwise independent of the GPU count.
 

@@ -93,22 +93,52 @@ def test_c_abi_rejects_bad_configs():
 
 # ---------------------------------------------------------------------------------------------
 # Sharded exchange on CPU (gloo): plan + all_gather layout + the hyper kernel's fixed-order sum.
+def wave_reduce(acc: np.ndarray) -> np.ndarray:
+    """numpy restatement of block_reduce's per-wave part (kernels.hip): (64, NS) lane values ->
+    (NS,) totals, with the device's addition order: v_permlane32_swap halving, v_permlane16_swap
+    halving, then a DPP row_ror 8/4/2/1 allreduce within 16-lane rows."""
+    NS = acc.shape[1]
+    H1, H2 = (NS + 1) // 2, ((NS + 1) // 2 + 1) // 2
+    w1 = np.zeros((64, H1))
+    for j in range(H1):
+        a = acc[:, j].copy()
+        b = acc[:, j + H1].copy() if j + H1 < NS else np.zeros(64)
+        a2, b2 = a.copy(), b.copy()
+        a2[32:], b2[:32] = b[:32], a[32:]
+        w1[:, j] = a2 + b2
+    w2 = np.zeros((64, H2))
+    for j in range(H2):
+        a = w1[:, j].copy()
+        b = w1[:, j + H2].copy() if j + H2 < H1 else np.zeros(64)
+        a2, b2 = a.copy(), b.copy()
+        for r in (1, 3):
+            a2[16 * r:16 * r + 16], b2[16 * (r - 1):16 * r] = b[16 * (r - 1):16 * r], a[16 * r:16 * r + 16]
+        w2[:, j] = a2 + b2
+    lanes = np.arange(64)
+    rot = lambda R: (lanes & ~15) | ((lanes + R) & 15)  # noqa: E731  (row_ror:R source lane)
+    for R in (8, 4, 2, 1):
+        w2 = w2 + w2[rot(R)]
+    out = np.zeros(NS)
+    for row in range(4):
+        for j in range(H2):
+            i1 = j + (H2 if row & 1 else 0)
+            idx = i1 + (H1 if row >> 1 else 0)
+            if i1 < H1 and idx < NS:
+                out[idx] = w2[16 * row, j]
+    return out
+
+
 def fixed_order_sum(units: np.ndarray, n_units_global: int, upr: int, world: int, chain: int, n_chains: int):
-    """numpy restatement of hyper_kernel's reduction order (kernels.hip): thread t of 256 sums
-    units t, t+256, ... sequentially; each 64-lane wave combines lanes by an xor butterfly; lane 0
-    of the 4 waves are added in wave order."""
-    stride = units.shape[-1]
+    """numpy restatement of hyper_body's reduction order (kernels.hip): thread t of 256 sums
+    units t, t+256, ... sequentially; each 64-lane wave reduces as wave_reduce(); the 4 waves'
+    totals are added in wave order.  units: gathered [world][chain][stride][units_per_rank]."""
+    stride = units.shape[2]
     acc = np.zeros((256, stride))
     for t in range(256):
         for u in range(t, n_units_global, 256):
             r, lu = divmod(u, upr)
-            acc[t] += units[r, chain, lu]
-    waves = []
-    for w in range(4):
-        v = acc[64 * w:64 * (w + 1)].copy()
-        for off in (32, 16, 8, 4, 2, 1):
-            v = v + v[np.arange(64) ^ off]
-        waves.append(v[0])
+            acc[t] += units[r, chain, :, lu]
+    waves = [wave_reduce(acc[64 * w:64 * (w + 1)]) for w in range(4)]
     return ((waves[0] + waves[1]) + waves[2]) + waves[3]
 
 
@@ -122,10 +152,10 @@ def _unit_partials(stats_per_customer: np.ndarray, begin: int, end: int, plan, n
         lo, hi = begin + b * 256, min(end, begin + (b + 1) * 256)
         if lo < hi:
             blocks[:, b] = stats_per_customer[:, lo:hi].sum(1)
-    units = np.zeros((n_chains, bpr // G, stride))
+    units = np.zeros((n_chains, stride, bpr // G))  # statistic-major, as clv_partials() exposes it
     for u in range(bpr // G):
         for bb in range(G):
-            units[:, u] += blocks[:, u * G + bb]
+            units[:, :, u] += blocks[:, u * G + bb]
     return units
 
 
@@ -144,7 +174,7 @@ def _worker(rank, world, port, n_global, q):
     local = torch.from_numpy(units.reshape(-1).copy())
     gathered = torch.zeros(local.numel() * world, dtype=torch.float64)
     D.exchange(local, gathered)
-    g = gathered.numpy().reshape(world, C, plan.units_per_rank, stride)
+    g = gathered.numpy().reshape(world, C, stride, plan.units_per_rank)
     sums = [fixed_order_sum(g, plan.n_units_global, plan.units_per_rank, world, c, C) for c in range(C)]
     q.put((rank, np.stack(sums), (b, e)))
     dist.destroy_process_group()

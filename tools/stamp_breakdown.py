@@ -40,6 +40,9 @@ def main(workload="c2", sweeps=1500, chains=None):
     print(f"  last block start:                       {us(rel[:, 5]):8.2f} us")
     print(f"  last block end -> tail start:           {us(st[:, 2] - st[:, 1]):8.2f} us")
     print(f"  tail (level-2 draw):                    {us(st[:, 3] - st[:, 2]):8.2f} us")
+    print(f"    tail: unit reduction                  {us(st[:, 6] - st[:, 2]):8.2f} us")
+    print(f"    tail: level-2 algebra (one lane)      {us(st[:, 7] - st[:, 6]):8.2f} us")
+    print(f"    tail: record + counters               {us(st[:, 3] - st[:, 7]):8.2f} us")
     # placement of the latest launch's workgroups: per CU (XCC, SE, CU) count and durations
     nb = -(-s.n // 256)
     wg = np.zeros(s.chains * nb * 4, np.uint64)
