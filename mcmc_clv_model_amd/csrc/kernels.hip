@@ -541,10 +541,10 @@ struct Cust {
   uint32_t gi;        // global customer index (Philox counter)
 };
 
-// Phase A (bi:193-227, bi:280-290): load, draw_z, draw_tau, log-posterior constants.
-template <int D, int K, bool REPLAY>
-__device__ __forceinline__ void cust_prepare(Cust<D, K>& u, const SweepArgs& a, int c, int64_t s, const double* H,
-                                             uint32_t k0, uint32_t k1, const double* tape, const double* exp_tab) {
+// Phase A1: the customer's loads (CBS row, covariates, state), issued before the workgroup's
+// exp-table barrier so their latency overlaps it.
+template <int D, int K>
+__device__ __forceinline__ void cust_load(Cust<D, K>& u, const SweepArgs& a, int c) {
   const Geometry& g = a.g;
   const int64_t i = u.i;
   u.tx = a.tx[i];
@@ -553,12 +553,19 @@ __device__ __forceinline__ void cust_prepare(Cust<D, K>& u, const SweepArgs& a, 
 #pragma unroll
   for (int k = 1; k < K; ++k) u.xr[k] = a.cov[(int64_t)(k - 1) * g.n + i];
   const int64_t ci = (int64_t)c * g.n + i;
-  const double lam = a.lam[ci];
-  const double mu = a.mu[ci];
-  u.lam = lam;
-  u.mu = mu;
+  u.lam = a.lam[ci];
+  u.mu = a.mu[ci];
   u.xm = (double)a.x[i];
   u.gi = (uint32_t)(g.shard_begin + i);
+}
+
+// Phase A2 (bi:193-227, bi:280-290): draw_z, draw_tau, log-posterior constants.
+template <int D, int K, bool REPLAY>
+__device__ __forceinline__ void cust_prepare(Cust<D, K>& u, const SweepArgs& a, int c, int64_t s, const double* H,
+                                             uint32_t k0, uint32_t k1, const double* tape, const double* exp_tab) {
+  const Geometry& g = a.g;
+  const int64_t i = u.i;
+  const double lam = u.lam, mu = u.mu;
   const double tx = u.tx, T = u.T;
 
   // ---- draw_z (bi:193-200)
@@ -579,7 +586,9 @@ __device__ __forceinline__ void cust_prepare(Cust<D, K>& u, const SweepArgs& a, 
   }
   const double ml = mu + lam;
   const double zz = ml * (T - tx);
-  const double e = exp(-zz);
+  // Philox mode: exp_fast, argument capped at 700 (exp(-700) ~ 1e-304 already makes
+  // p(alive) < 2^-53, the smallest nonzero u_z, as exp(-zz) underflowing to 0 does)
+  const double e = REPLAY ? exp(-zz) : exp_fast(-min700(zz), exp_tab);
   const double p = (ml * e) / (ml * e + mu * (1.0 - e));
   const bool z = u_z < p;
   u.z = z;
@@ -595,7 +604,9 @@ __device__ __forceinline__ void cust_prepare(Cust<D, K>& u, const SweepArgs& a, 
     if constexpr (REPLAY) uu = v_tau; else uu = u53(rz, rw);
     const double ml_tx = min700(ml * tx);
     const double ml_T = min700(ml * T);
-    tau = -log((1 - uu) * exp(-ml_tx) + uu * exp(-ml_T)) / ml;
+    const double e_tx = REPLAY ? exp(-ml_tx) : exp_fast(-ml_tx, exp_tab);  // both capped at 700 (bi:223)
+    const double e_T = REPLAY ? exp(-ml_T) : exp_fast(-ml_T, exp_tab);
+    tau = -log((1 - uu) * e_tx + uu * e_T) / ml;
   }
   u.tau = tau;
 
@@ -651,12 +662,14 @@ __device__ __forceinline__ void mh_step(Cust<D, K>& u, double s00, double s11, f
 template <int D, int K, bool REPLAY, int NS>
 __device__ __forceinline__ void cust_finish(Cust<D, K>& u, const SweepArgs& a, int c, int64_t s, bool stored,
                                             const double* H, uint32_t k0, uint32_t k1, const double* tape,
-                                            double (&acc)[NS]) {
+                                            const double* exp_tab, double (&acc)[NS]) {
   constexpr int NXY = K * D;
   const Geometry& g = a.g;
   const int64_t i = u.i;
-  double lam = exp(u.ll);  // bi:337-338
-  double mu = exp(u.lm);
+  // bi:337-338 (state back to natural scale).  Replay reproduces the reference's exp/log round
+  // trips (quirk Q5) bit for bit; Philox mode takes log(exp(ll)) = ll (equal to within an ulp).
+  double lam = REPLAY ? exp(u.ll) : exp_fast(u.ll, exp_tab);
+  double mu = REPLAY ? exp(u.lm) : exp_fast(u.lm, exp_tab);
   double eta = 1.0, Y[D];
   const bool z = u.z;
   if constexpr (D == 3) {
@@ -674,14 +687,16 @@ __device__ __forceinline__ void cust_finish(Cust<D, K>& u, const SweepArgs& a, i
     }
     eta = exp(post_mean + H[H_SQRT_POSTVAR] * zeta);
     // tri: level 2 sees log(lambda) before the storage round trip (tri:529-536 before :542)
-    Y[0] = log(lam);
-    Y[1] = log(mu);
+    Y[0] = REPLAY ? log(lam) : u.ll;
+    Y[1] = REPLAY ? log(mu) : u.lm;
     Y[2] = log(eta);
   }
   double lik = 0.0;
   if (stored) {
-    lam = exp(log(lam));  // quirk Q5 (bi:405-406)
-    mu = exp(log(mu));
+    if constexpr (REPLAY) {
+      lam = exp(log(lam));  // quirk Q5 (bi:405-406)
+      mu = exp(log(mu));
+    }
     const int64_t dr = draw_index(s, g);
     if (a.level1) {
       double* o = a.level1 + (((int64_t)c * g.n_draws + dr) * g.n + i) * (D + 2);
@@ -691,7 +706,7 @@ __device__ __forceinline__ void cust_finish(Cust<D, K>& u, const SweepArgs& a, i
       o[3] = z ? 1.0 : 0.0;
       if constexpr (D == 3) o[4] = eta;
     }
-    const double lgl = log(lam), lgm = log(mu);
+    const double lgl = REPLAY ? log(lam) : u.ll, lgm = REPLAY ? log(mu) : u.lm;
     lik = (u.xm * lgl + u.lc.omz * lgm) - (lam + mu) * u.lc.w;  // bi:423-427
     if (a.sums) {
       double* sm = a.sums + (int64_t)c * CLV_N_SUM_STATS * g.n + i;
@@ -710,8 +725,8 @@ __device__ __forceinline__ void cust_finish(Cust<D, K>& u, const SweepArgs& a, i
   }
   if constexpr (D == 2) {
     // bi: the next level-2 draw uses log of the carried state (bi:393)
-    Y[0] = log(lam);
-    Y[1] = log(mu);
+    Y[0] = REPLAY ? log(lam) : u.ll;
+    Y[1] = REPLAY ? log(mu) : u.lm;
   }
   const int64_t ci = (int64_t)c * g.n + i;
   a.lam[ci] = lam;
@@ -741,10 +756,10 @@ __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
   __shared__ double red[BLOCK / 64][NS];
   __shared__ double tot[NS];
   __shared__ double exp_tab[64];
-  if constexpr (!REPLAY) {
-    load_exp_table(exp_tab);
-    __syncthreads();
-  }
+  // the exp table's global load is issued first; it is stored to LDS (and the barrier taken)
+  // after the customer's own loads are in flight
+  double tab_v = 0.0;
+  if (!REPLAY && threadIdx.x < 64) tab_v = EXP2_TAB64[threadIdx.x];
 
   const Geometry& g = a.g;
   const int c = blockIdx.y;
@@ -761,31 +776,6 @@ __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
     CLV_WG_STAMP(a.stamps, (int64_t)c * g.nb_local + b, 0);
     CLV_WG_STAMP(a.stamps, (int64_t)c * g.nb_local + b, 2);
     CLV_WG_STAMP(a.stamps, (int64_t)c * g.nb_local + b, 3);
-  }
-
-  // ---- the next level-2 draw's Philox variates (independent of the statistics): computed by
-  // the last wavefront of the chain's last workgroup — the partially filled one — so the draw's
-  // serial tail only loads them.  Written with sc1 (write-through) stores.
-  if constexpr (!REPLAY) {
-    if (a.hvar_out && !a.init && b == g.nb_local - 1 && (int)(threadIdx.x >> 6) == NT / 64 - 1) {
-      const int l = threadIdx.x & 63;
-      const int64_t hs = (D == 2) ? s + 1 : s;
-      uint32_t k0, k1;
-      chain_key(a.r.seed, (int64_t)a.r.chain_first + c, &k0, &k1);
-      double v = 0.0;
-      int slot = -1;
-      if (l < D * (D - 1) / 2) {
-        v = hyper_normal(k0, k1, HSLOT_NORMAL0 + l, (uint32_t)hs);
-        slot = l;
-      } else if (l >= 8 && l < 8 + D * K) {
-        v = hyper_normal(k0, k1, HSLOT_BETA_NORMAL0 + (l - 8), (uint32_t)hs);
-        slot = l;
-      } else if (l >= 40 && l < 40 + D) {
-        v = chi2_draw(k0, k1, (uint32_t)hs, l - 40, a.h.nu_n - D + 1 + (l - 40));
-        slot = 3 + (l - 40);
-      }
-      if (slot >= 0) __hip_atomic_store(a.hvar_out + (int64_t)c * HV + slot, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
   }
 
   Cust<D, K> cu;
@@ -822,7 +812,37 @@ __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
 #pragma unroll
         for (int r = p; r < D; ++r) acc[t++] += Y[p] * Y[r];
     }
-  } else if (cu.active) {
+  }
+  if (!a.init && g.n > 0) cust_load(cu, a, c);  // inactive lanes load a clamped valid row
+  if (!REPLAY && threadIdx.x < 64) exp_tab[threadIdx.x] = tab_v;
+  __syncthreads();
+
+  // ---- the next level-2 draw's Philox variates (independent of the statistics): computed by
+  // the last wavefront of the chain's last workgroup — the partially filled one — so the draw's
+  // serial tail only loads them.  Written with sc1 (write-through) stores.
+  if constexpr (!REPLAY) {
+    if (a.hvar_out && !a.init && b == g.nb_local - 1 && (int)(threadIdx.x >> 6) == NT / 64 - 1) {
+      const int l = threadIdx.x & 63;
+      const int64_t hs = (D == 2) ? s + 1 : s;
+      uint32_t k0, k1;
+      chain_key(a.r.seed, (int64_t)a.r.chain_first + c, &k0, &k1);
+      double v = 0.0;
+      int slot = -1;
+      if (l < D * (D - 1) / 2) {
+        v = hyper_normal(k0, k1, HSLOT_NORMAL0 + l, (uint32_t)hs);
+        slot = l;
+      } else if (l >= 8 && l < 8 + D * K) {
+        v = hyper_normal(k0, k1, HSLOT_BETA_NORMAL0 + (l - 8), (uint32_t)hs);
+        slot = l;
+      } else if (l >= 40 && l < 40 + D) {
+        v = chi2_draw(k0, k1, (uint32_t)hs, l - 40, a.h.nu_n - D + 1 + (l - 40));
+        slot = 3 + (l - 40);
+      }
+      if (slot >= 0) __hip_atomic_store(a.hvar_out + (int64_t)c * HV + slot, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+
+  if (!a.init && cu.active) {
     const double* H = a.hyper + (int64_t)c * HS;
     uint32_t k0 = 0, k1 = 0;
     const double* tape = nullptr;
@@ -874,7 +894,7 @@ __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
         }
       }
     }
-    cust_finish<D, K, REPLAY, NS>(cu, a, c, s, stored, H, k0, k1, tape, acc);
+    cust_finish<D, K, REPLAY, NS>(cu, a, c, s, stored, H, k0, k1, tape, exp_tab, acc);
   }
 
   block_reduce<NS>(acc, red, tot);
@@ -987,18 +1007,11 @@ __global__ void debug_variates_kernel(uint64_t seed, int chain, uint32_t sweep, 
   const u32x4 re = customer_block(k0, k1, (uint32_t)i, sweep, SLOT_ETA);
   ez[i] = sqrt(-2.0 * log(u53_open0(re.x, re.y))) * cospi(2.0 * u53(re.z, re.w));
   const SlotPhilox ph(k0, k1, (uint32_t)i, sweep);
-  for (int q = 0; q * MH_CHUNK_STEPS < S; ++q) {
-    float a[4], b[4], lu[4];
-    mh_chunk_variates(ph, (uint32_t)q, a, b, lu);
-    for (int k = 0; k < MH_CHUNK_STEPS && q * MH_CHUNK_STEPS + k < S; ++k) {
-      const int j = q * MH_CHUNK_STEPS + k;
-      const int w = MH_WORDS * j + 4;  // accept-uniform word of step j
-      const u32x4 r = ph(SLOT_MH0 + (uint32_t)(w / 4));
-      const uint32_t wa = (w % 4 == 0) ? r.x : (w % 4 == 1) ? r.y : (w % 4 == 2) ? r.z : r.w;
-      tl[(int64_t)j * n + i] = a[k];
-      tm[(int64_t)j * n + i] = b[k];
-      ua[(int64_t)j * n + i] = uf32(wa);
-    }
+  for (int j = 0; j < S; ++j) {
+    const u32x4 r = ph(SLOT_MH0 + (uint32_t)j);
+    tl[(int64_t)j * n + i] = t3_f32(uf32(r.x), angle_hi(r.z));
+    tm[(int64_t)j * n + i] = t3_f32(uf32(r.y), angle_lo(r.z));
+    ua[(int64_t)j * n + i] = uf32(r.w);
   }
 }
 

@@ -45,7 +45,7 @@ CLV_HD u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
 enum : uint32_t { STREAM_CUSTOMER = 0u, STREAM_HYPER = 1u };
 
 // Customer-stream slots (counter word 2).
-enum : uint32_t { SLOT_ZTAU = 0u, SLOT_ETA = 1u, SLOT_MH0 = 2u };  // MH chunk q: SLOT_MH0+5q .. +5q+4
+enum : uint32_t { SLOT_ZTAU = 0u, SLOT_ETA = 1u, SLOT_MH0 = 2u };  // MH step j: block SLOT_MH0 + j
 
 // Hyper-stream slots (counter word 0; word 1 = sweep).
 enum : uint32_t { HSLOT_NORMAL0 = 0u, HSLOT_BETA_NORMAL0 = 4u, HSLOT_GAMMA0 = 64u, HSLOT_GAMMA_STRIDE = 256u };
@@ -120,40 +120,35 @@ __device__ __forceinline__ float uf32(uint32_t w) {
 __device__ __forceinline__ float ln_f32(float u) {  // natural log via v_log_f32 (log2)
   return __builtin_amdgcn_logf(u) * 0.69314718055994530942f;
 }
-// Student-t(3) from two words by Bailey's trigonometric form of the polar method (Bailey 1994,
-// Math. Comp. 62:779-781): R^2 = nu (U^(-2/nu) - 1) is the squared radius of a spherical
-// bivariate t_nu, so R cos(2 pi V) is exactly t_nu.  Four hardware transcendentals, no rejection.
-__device__ __forceinline__ float t3_f32(uint32_t wu, uint32_t wv) {
-  const float p = __builtin_amdgcn_exp2f(-(2.0f / 3.0f) * __builtin_amdgcn_logf(uf32(wu)));  // U^(-2/3)
+// Student-t(3) by Bailey's trigonometric form of the polar method (Bailey 1994, Math. Comp.
+// 62:779-781): R^2 = nu (U^(-2/nu) - 1) is the squared radius of a spherical bivariate t_nu, so
+// R cos(2 pi V) is exactly t_nu.  Four hardware transcendentals, no rejection.  The radius
+// uniform u is a full 32-bit word; the angle v (revolutions, v_cos_f32) has 16-bit resolution —
+// a symmetric lattice of angles, so the proposal stays symmetric and MH stays exact.
+__device__ __forceinline__ float t3_f32(float u, float v) {
+  const float p = __builtin_amdgcn_exp2f(-(2.0f / 3.0f) * __builtin_amdgcn_logf(u));  // U^(-2/3)
   const float r = __builtin_amdgcn_sqrtf(3.0f * (p - 1.0f));
-  return r * __builtin_amdgcn_cosf(uf32(wv));  // v_cos_f32 takes revolutions
+  return r * __builtin_amdgcn_cosf(v);
 }
+// The two 16-bit angles of one word, in revolutions: high half -> t_l, low half -> t_m.
+__device__ __forceinline__ float angle_hi(uint32_t w) { return (float)(w & 0xffff0000u) * 0x1.0p-32f; }
+__device__ __forceinline__ float angle_lo(uint32_t w) { return (float)(w << 16) * 0x1.0p-32f; }
 
-// Words of the MH steps: step j uses words 5j .. 5j+4 of the customer's MH word stream, word w =
-// lane (w % 4) of Philox block slot SLOT_MH0 + w / 4.  Chunk q (steps 4q .. 4q+3) = blocks
-// SLOT_MH0 + 5q .. 5q+4.  Step words: (U, V) of t_l, (U, V) of t_m, accept uniform.
-constexpr int MH_WORDS = 5;
+// Words of the MH steps: step j uses the four words of Philox block SLOT_MH0 + j:
+// x = radius uniform of t_l, y = radius uniform of t_m, z = the two angles (16 bits each),
+// w = accept uniform.  Chunk q = steps 4q .. 4q+3.
 constexpr int MH_CHUNK_STEPS = 4;
-constexpr int MH_CHUNK_BLOCKS = 5;
 
 // One chunk's variates: t_l, t_m and log(U_accept) of 4 consecutive MH steps.
 template <class PH>
 __device__ __forceinline__ void mh_chunk_variates(const PH& ph, uint32_t q, float (&t_l)[4], float (&t_m)[4],
                                                   float (&log_u)[4]) {
-  uint32_t w[20];
-#pragma unroll
-  for (int b = 0; b < MH_CHUNK_BLOCKS; ++b) {
-    const u32x4 r = ph(SLOT_MH0 + (uint32_t)MH_CHUNK_BLOCKS * q + (uint32_t)b);
-    w[4 * b] = r.x;
-    w[4 * b + 1] = r.y;
-    w[4 * b + 2] = r.z;
-    w[4 * b + 3] = r.w;
-  }
 #pragma unroll
   for (int i = 0; i < MH_CHUNK_STEPS; ++i) {
-    t_l[i] = t3_f32(w[5 * i], w[5 * i + 1]);
-    t_m[i] = t3_f32(w[5 * i + 2], w[5 * i + 3]);
-    log_u[i] = ln_f32(uf32(w[5 * i + 4]));
+    const u32x4 r = ph(SLOT_MH0 + (uint32_t)MH_CHUNK_STEPS * q + (uint32_t)i);
+    t_l[i] = t3_f32(uf32(r.x), angle_hi(r.z));
+    t_m[i] = t3_f32(uf32(r.y), angle_lo(r.z));
+    log_u[i] = ln_f32(uf32(r.w));
   }
 }
 

@@ -74,36 +74,40 @@ def hyper_block(seed, chain, slot, sweep):
     return philox4x32_10(np.array([slot, sweep, 0, STREAM_HYPER], dtype=np.uint32), k0, k1)
 
 
-def t3_f32(wu, wv):
+def t3_f32(u, v):
     """Student-t(3) by Bailey's trigonometric polar form: sqrt(3 (U^(-2/3) - 1)) cos(2 pi V)
-    (csrc/philox.h:t3_f32; fp32 like the device's v_log/v_exp/v_sqrt/v_cos)."""
-    p = np.exp2(np.float32(-2.0 / 3.0) * np.log2(uf32(wu))).astype(np.float32)
+    (csrc/philox.h:t3_f32; fp32 like the device's v_log/v_exp/v_sqrt/v_cos); v in revolutions."""
+    p = np.exp2(np.float32(-2.0 / 3.0) * np.log2(u)).astype(np.float32)
     r = np.sqrt(np.float32(3.0) * (p - np.float32(1.0))).astype(np.float32)
-    return (r * np.cos(uf32(wv).astype(np.float64) * (2.0 * np.pi))).astype(np.float32)
+    return (r * np.cos(v.astype(np.float64) * (2.0 * np.pi))).astype(np.float32)
 
 
-MH_WORDS, MH_CHUNK_STEPS, MH_CHUNK_BLOCKS = 5, 4, 5
+def angle_hi(w):
+    return ((w & np.uint32(0xFFFF0000)).astype(np.float32) * np.float32(2.0 ** -32)).astype(np.float32)
 
 
-def mh_words(seed, chain, cust, sweep, n_steps):
-    """(5 * n_steps, n) uint32: the MH word stream, word w = lane w % 4 of block SLOT_MH0 + w // 4."""
-    n_blocks = -(-MH_WORDS * n_steps // 4)
-    w = np.empty((4 * n_blocks, len(cust)), np.uint32)
-    for b in range(n_blocks):
-        w[4 * b:4 * b + 4] = customer_blocks(seed, chain, cust, sweep, SLOT_MH0 + b).T
-    return w[:MH_WORDS * n_steps]
+def angle_lo(w):
+    return ((w << np.uint32(16)).astype(np.uint32).astype(np.float32) * np.float32(2.0 ** -32)).astype(np.float32)
 
 
 def sweep_variates(seed, chain, sweep, n, n_steps):
-    """The Philox-mode variates of one sweep for customers 0..n-1 (see csrc/philox.h)."""
+    """The Philox-mode variates of one sweep for customers 0..n-1 (see csrc/philox.h): MH step j
+    uses block SLOT_MH0 + j = (radius of t_l, radius of t_m, two 16-bit angles, accept uniform)."""
     cust = np.arange(n)
     r = customer_blocks(seed, chain, cust, sweep, SLOT_ZTAU)
     out = dict(u_z=u53(r[:, 0], r[:, 1]), u_tau=u53(r[:, 2], r[:, 3]),
                e_alive=-np.log(u53_open0(r[:, 2], r[:, 3])))
     re = customer_blocks(seed, chain, cust, sweep, SLOT_ETA)
     out["eta_z"] = np.sqrt(-2.0 * np.log(u53_open0(re[:, 0], re[:, 1]))) * np.cos(2.0 * np.pi * u53(re[:, 2], re[:, 3]))
-    w = mh_words(seed, chain, cust, sweep, n_steps).reshape(n_steps, MH_WORDS, n)
-    out.update(t_l=t3_f32(w[:, 0], w[:, 1]), t_m=t3_f32(w[:, 2], w[:, 3]), u_acc=uf32(w[:, 4]))
+    tl = np.empty((n_steps, n), np.float32)
+    tm = np.empty((n_steps, n), np.float32)
+    ua = np.empty((n_steps, n), np.float32)
+    for j in range(n_steps):
+        w = customer_blocks(seed, chain, cust, sweep, SLOT_MH0 + j)
+        tl[j] = t3_f32(uf32(w[:, 0]), angle_hi(w[:, 2]))
+        tm[j] = t3_f32(uf32(w[:, 1]), angle_lo(w[:, 2]))
+        ua[j] = uf32(w[:, 3])
+    out.update(t_l=tl, t_m=tm, u_acc=ua)
     return out
 
 
