@@ -172,6 +172,12 @@ __device__ __forceinline__ void wg_stamp(unsigned long long* st, int64_t wg, int
 #define CLV_STAMP(st, s, k, is_min) ((void)0)
 #endif
 
+__device__ __forceinline__ int64_t uniform_i64(int64_t v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)v >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
 __device__ __forceinline__ bool is_stored(int64_t s, const Geometry& g) {
   return s > g.burnin && s <= (int64_t)g.burnin + g.mcmc && ((s - 1 - g.burnin) % g.thin) == 0;
 }
@@ -747,6 +753,8 @@ __device__ __forceinline__ void cust_finish(Cust<D, K>& u, const SweepArgs& a, i
 // One workgroup = one statistics block of BLOCK customers of one chain, one customer per lane.
 // (Two interleaved customers per lane for ILP at CDNOW size measured slower — 35 vs 23 us/sweep —
 // and would tie the statistics' summation order to the lane mapping.)
+static_assert(BLOCK == EXP_TAB_N, "the sweep kernel stages the exp table with one entry per lane");
+
 template <int D, int K, bool REPLAY>
 __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
   constexpr int NT = BLOCK;
@@ -755,16 +763,18 @@ __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
   constexpr int NS = NXY + NYY + 1;
   __shared__ double red[BLOCK / 64][NS];
   __shared__ double tot[NS];
-  __shared__ double exp_tab[64];
+  __shared__ double exp_tab[EXP_TAB_N];
   // the exp table's global load is issued first; it is stored to LDS (and the barrier taken)
   // after the customer's own loads are in flight
   double tab_v = 0.0;
-  if (!REPLAY && threadIdx.x < 64) tab_v = EXP2_TAB64[threadIdx.x];
+  if (!REPLAY) tab_v = EXP2_TAB[threadIdx.x];  // BLOCK == EXP_TAB_N
 
   const Geometry& g = a.g;
   const int c = blockIdx.y;
   const int b = blockIdx.x;
-  const int64_t s = a.init ? 0 : __hip_atomic_load(&a.ctrl->cur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  // the sweep index is uniform: readfirstlane keeps it (and the Philox words derived from it) in
+  // scalar registers — a vector atomic load alone would make it look divergent to the compiler
+  const int64_t s = a.init ? 0 : uniform_i64(__hip_atomic_load(&a.ctrl->cur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + 1;
   const bool stored = !a.init && is_stored(s, g);
 
   double acc[NS];
@@ -814,7 +824,7 @@ __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
     }
   }
   if (!a.init && g.n > 0) cust_load(cu, a, c);  // inactive lanes load a clamped valid row
-  if (!REPLAY && threadIdx.x < 64) exp_tab[threadIdx.x] = tab_v;
+  if (!REPLAY) exp_tab[threadIdx.x] = tab_v;
   __syncthreads();
 
   // ---- the next level-2 draw's Philox variates (independent of the statistics): computed by
@@ -1051,8 +1061,8 @@ __global__ void debug_hyper_variates_kernel(uint64_t seed, int chain, uint32_t s
 }
 
 __global__ void debug_exp_kernel(const double* x, int64_t n, double* out) {
-  __shared__ double tab[64];
-  load_exp_table(tab);
+  __shared__ double tab[EXP_TAB_N];
+  for (int j = threadIdx.x; j < EXP_TAB_N; j += blockDim.x) tab[j] = EXP2_TAB[j];
   __syncthreads();
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) out[i] = exp_fast(x[i], tab);

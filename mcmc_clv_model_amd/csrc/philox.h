@@ -80,15 +80,22 @@ struct SlotPhilox {
     r1w = (uint32_t)p0;
     p1r2 = (uint64_t)0xCD9E8D57u * r1z;
   }
+  // `slot` must be uniform across the wavefront (it is at every call site: a loop counter):
+  // round 1's M1 * slot and round 2's M0 product then run on the scalar unit.
   CLV_HD u32x4 operator()(uint32_t slot) const {
-    // round 1 (key k)
+#if defined(__HIP_DEVICE_COMPILE__)
+    slot = __builtin_amdgcn_readfirstlane(slot);
+#endif
+    // round 1 (key k): words x, y are uniform (plain xor: scalar unit)
     const uint64_t p1 = (uint64_t)0xCD9E8D57u * slot;
-    u32x4 c{xor3((uint32_t)(p1 >> 32), sweep, k0), (uint32_t)p1, r1z, r1w};
+    u32x4 c{(uint32_t)(p1 >> 32) ^ sweep ^ k0, (uint32_t)p1, r1z, r1w};
     uint32_t a0 = k0 + 0x9E3779B9u, a1 = k1 + 0xBB67AE85u;
-    // round 2: the second product is slot-independent
+    // round 2: M0 * x is uniform, M1 * z (= p1r2) is slot-independent and hoisted; the uniform
+    // parts of each xor are combined first, so each lane pays one v_xor
     {
       const uint64_t q0 = (uint64_t)0xD2511F53u * c.x;
-      c = u32x4{xor3((uint32_t)(p1r2 >> 32), c.y, a0), (uint32_t)p1r2, xor3((uint32_t)(q0 >> 32), c.w, a1), (uint32_t)q0};
+      const uint32_t ux = c.y ^ a0, uz = (uint32_t)(q0 >> 32) ^ a1;
+      c = u32x4{(uint32_t)(p1r2 >> 32) ^ ux, (uint32_t)p1r2, uz ^ c.w, (uint32_t)q0};
       a0 += 0x9E3779B9u;
       a1 += 0xBB67AE85u;
     }
