@@ -83,6 +83,14 @@ def exchange(local, gathered, group=None) -> None:
     dist.all_gather_into_tensor(gathered, local, group=group)
 
 
+class _DeviceArray:
+    """A float64 device buffer owned by the HIP library, exposed to torch without a copy."""
+
+    def __init__(self, ptr: int, n: int):
+        self.__cuda_array_interface__ = dict(shape=(int(n),), typestr="<f8", data=(int(ptr), False), version=3,
+                                             strides=None)
+
+
 class ShardedSampler:
     """This rank's shard of a problem on its GPU; sweeps with one all-gather per sweep.
 
@@ -115,8 +123,10 @@ class ShardedSampler:
                             world_size=world, rank=rank, blocks_per_rank=self.plan.blocks_per_rank,
                             blocks_per_unit=self.plan.blocks_per_unit, stream=self.base_stream, prior=prior)
         self.n = self.s.n
-        _, nd, _ = self.s.partials()
-        self.local = torch.zeros(nd, dtype=torch.float64, device=f"cuda:{device}")
+        ptr, nd, _ = self.s.partials()
+        # zero-copy view of the sampler's own unit-partial buffer: the sweep (or group) kernel
+        # writes it, the all-gather reads it — no device-to-device copy node per sweep
+        self.local = torch.as_tensor(_DeviceArray(ptr, nd), device=f"cuda:{device}")
         self.gathered = torch.zeros(nd * world, dtype=torch.float64, device=f"cuda:{device}")
         self.cur = self.stream  # the stream launches go to (a capture stream while capturing)
         self.D = p_global.D
@@ -124,7 +134,6 @@ class ShardedSampler:
             self._exchange_and_hyper()
 
     def _exchange_and_hyper(self) -> None:
-        self.s.copy_partials(self.local.data_ptr())
         with self.torch.cuda.stream(self.cur):
             exchange(self.local, self.gathered, self.group)
         self.s.hyper(self.gathered.data_ptr())
