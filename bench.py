@@ -54,8 +54,8 @@ def algorithmic_bytes(D: int, K: int, stored_frac: float, draw_sink: str) -> flo
 
 def committed_traffic(workload: str, sharded: bool):
     """HBM bytes per sweep-kernel launch from the committed rocprofv3 PMC summary of this workload
-    (profiles/*_summary.json written by tools/summarize_profile.py): FETCH_SIZE + WRITE_SIZE,
-    uncorrected (see DESIGN.md §Roofline for the gfx950 FETCH_SIZE caveat); None if absent."""
+    (profiles/*_summary.json written by tools/summarize_profile.py): FETCH_SIZE and WRITE_SIZE
+    corrected by the calibration kernels of tools/calib_fetch.hip; None if absent."""
     import glob
     if sharded:
         return None
@@ -66,9 +66,10 @@ def committed_traffic(workload: str, sharded: bool):
         except Exception:
             continue
         for name, k in d.get("kernels", {}).items():
-            if "sweep_kernel" in name and "traffic_bytes_uncorrected" in k:
-                best = dict(bytes_per_launch=round(k["traffic_bytes_uncorrected"]), source=os.path.basename(path),
-                            counters="FETCH_SIZE+WRITE_SIZE (x1024, uncorrected)")
+            if "sweep_kernel" in name and "traffic_bytes" in k:
+                best = dict(bytes_per_launch=round(k["traffic_bytes"]), source=os.path.basename(path),
+                            counters="FETCH_SIZE x %.2f + WRITE_SIZE x %.2f (calibrated, tools/calib_fetch.hip)"
+                                     % (k["traffic_correction"]["read"], k["traffic_correction"]["write"]))
     return best
 
 

@@ -3,9 +3,10 @@
 copy the rocprofv3 --stats table next to it.
 
 Per kernel: average duration (kernel-trace), FETCH_SIZE / WRITE_SIZE per dispatch (KB as reported
-by rocprofv3; gfx950 note in DESIGN.md: FETCH_SIZE under-counts wide streaming reads by 2x and is
-uncalibrated for 4/8-B-per-lane loads), VALU instructions and active cycles per wave, waves, and
-the effective clock from GRBM_GUI_ACTIVE.
+by rocprofv3), HBM traffic corrected with the calibration kernels of tools/calib_fetch.hip (known
+byte counts at 4/8/16 B per lane: on gfx950 FETCH_SIZE reports 1/2 of the bytes read, WRITE_SIZE
+all bytes written — MI355X_MICROARCH.md "HBM"), VALU instructions and active cycles per wave,
+waves, and the effective clock from GRBM_GUI_ACTIVE.
 """
 import csv
 import json
@@ -26,12 +27,33 @@ def mean_counter(path, counter):
     return {k: statistics.mean(v) for k, v in out.items()}
 
 
+def calibration(prof):
+    """bytes / counter-bytes for reads (worst case over 4/8/16 B per lane) and 8-B writes."""
+    out = {}
+    for counter, kern in (("FETCH_SIZE", ("read4", "read8", "read16")), ("WRITE_SIZE", ("write8",))):
+        path = os.path.join(prof, f"calib_{counter}", "run_counter_collection.csv")
+        if not os.path.exists(path):
+            return None
+        per = {}
+        for r in csv.DictReader(open(path)):
+            name = r["Kernel_Name"].split("(")[0]
+            if name in kern and r["Counter_Name"] == counter:
+                per.setdefault(name, []).append(float(r["Counter_Value"]) * 1024)
+        out[counter] = {k: (512 << 20) / statistics.mean(v) for k, v in per.items()}
+    return out
+
+
 def main(tag, prof=os.path.join(ROOT, "gpurun_out", "prof"), bench_log=None):
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
     stats = list(csv.DictReader(open(os.path.join(prof, "trace", "run_kernel_stats.csv"))))
     shutil.copy(os.path.join(prof, "trace", "run_kernel_stats.csv"), os.path.join(ROOT, "profiles", f"{tag}_kernel_stats.csv"))
     trace = list(csv.DictReader(open(os.path.join(prof, "trace", "run_kernel_trace.csv"))))
     res = {"tag": tag, "kernels": {}}
+    cal = calibration(prof)
+    if cal:
+        res["calibration"] = cal
+    f_read = cal["FETCH_SIZE"]["read8"] if cal else 2.0   # guide: FETCH_SIZE = 1/2 of the bytes read
+    f_write = cal["WRITE_SIZE"]["write8"] if cal else 1.0
     fetch = mean_counter(os.path.join(prof, "fetch_size", "run_counter_collection.csv"), "FETCH_SIZE")
     write = mean_counter(os.path.join(prof, "write_size", "run_counter_collection.csv"), "WRITE_SIZE")
     vpath = os.path.join(prof, "sq_insts_valu", "run_counter_collection.csv")
@@ -54,6 +76,8 @@ def main(tag, prof=os.path.join(ROOT, "gpurun_out", "prof"), bench_log=None):
             k["write_size_kb"] = write[name]
         if name in fetch and name in write:
             k["traffic_bytes_uncorrected"] = (fetch[name] + write[name]) * 1024
+            k["traffic_bytes"] = (fetch[name] * f_read + write[name] * f_write) * 1024
+            k["traffic_correction"] = dict(read=f_read, write=f_write)
         if name in valu["SQ_WAVES"]:
             waves = valu["SQ_WAVES"][name]
             k["waves"] = waves
