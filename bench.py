@@ -73,6 +73,27 @@ def committed_traffic(workload: str, sharded: bool):
     return best
 
 
+VALU_PEAK_WAVE_INSTS = 1024 * 2.4e9 / 4  # 256 CUs x 4 SIMDs, one wave64 fp64/int64 VALU op per 4 cycles
+
+
+def committed_valu(workload: str, sharded: bool):
+    """VALU wave-instructions per sweep-kernel launch (SQ_INSTS_VALU / SQ_WAVES x waves) from the
+    committed rocprofv3 summary of this workload; None if absent."""
+    import glob
+    if sharded:
+        return None
+    best = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{workload}_*summary.json"))):
+        try:
+            d = json.load(open(path))
+        except Exception:
+            continue
+        for name, k in d.get("kernels", {}).items():
+            if "sweep_kernel" in name and "valu_insts_per_wave" in k:
+                best = dict(wave_insts_per_launch=k["valu_insts_per_wave"] * k["waves"], source=os.path.basename(path))
+    return best
+
+
 def load_workload(name: str, world: int = 1):
     """CBS of a workload.  CDNOW: the committed CBS columns (weak scaling: one copy per rank).
     Synthetic: mcmc_clv_model_amd.data.synthetic_cbs with n per GPU (c5 weak scaling: n x world)."""
@@ -250,6 +271,13 @@ def main():
                             sweep_kernel_us=round(t_launch * 1e6, 3), timed_launches=kt["sweep_launches"])
             if kt["hyper_launches"]:
                 roofline["hyper_kernel_us"] = round(kt["hyper_ms"] / kt["hyper_launches"] * 1e3, 3)
+            v = committed_valu(a.workload, sharded)
+            if v:  # the binding resource: VALU issue, not HBM
+                ach = v["wave_insts_per_launch"] / t_launch
+                roofline["valu"] = dict(achieved=round(ach / 1e9, 2), peak=round(VALU_PEAK_WAVE_INSTS / 1e9, 1),
+                                        unit="G wave-instructions/s", frac=round(ach / VALU_PEAK_WAVE_INSTS, 4),
+                                        source=v["source"],
+                                        note="peak = 1,024 SIMDs x 2.4 GHz / 4 cycles (fp64-rate VALU issue)")
 
     if rank == 0:
         cpu = None
