@@ -208,7 +208,8 @@ def main():
 
     df, D, covs, chains, burnin, mcmc, thin, sink = load_workload(a.workload, world)
     total = a.warmup + a.steps + (0 if a.no_kernel_timing else min(a.steps, a.timing_steps))
-    mcmc = max(mcmc, total - burnin)
+    mcmc_workload = mcmc
+    mcmc = max(mcmc, total - burnin)  # draw buffers also cover the sweeps of the roofline pass
     n_total = len(df)
     if not sharded:
         p = build_problem(df, covs, D)
@@ -265,10 +266,14 @@ def main():
             t_launch = kt["sweep_ms"] / kt["sweep_launches"] * 1e-3
             achieved = bpu * chains * n_local / t_launch / 1e9
             roofline = dict(bound="hbm", achieved=round(achieved, 3), peak=HBM_PEAK_GBS, unit="GB/s",
-                            frac=round(achieved / HBM_PEAK_GBS, 6), traffic=committed_traffic(a.workload, sharded),
+                            frac=round(achieved / HBM_PEAK_GBS, 6), traffic=None,
                             kernel="sweep_kernel (incl. fused level-2 tail)" if not sharded else "sweep_kernel",
                             bytes_per_unit=round(bpu, 3), units_per_launch=chains * n_local,
                             sweep_kernel_us=round(t_launch * 1e6, 3), timed_launches=kt["sweep_launches"])
+            tr = committed_traffic(a.workload, sharded)
+            if tr:
+                roofline["traffic"] = tr["bytes_per_launch"]  # HBM bytes per launch (calibrated PMC)
+                roofline["traffic_source"] = f"{tr['source']}: {tr['counters']}"
             if kt["hyper_launches"]:
                 roofline["hyper_kernel_us"] = round(kt["hyper_ms"] / kt["hyper_launches"] * 1e3, 3)
             v = committed_valu(a.workload, sharded)
@@ -294,7 +299,7 @@ def main():
                    f"tests/golden/cdnow_{WORKLOADS[a.workload][1]}_cbs.npz)")
                   + ("" if world == 1 else f", tiled x{world} (one copy per rank)")),
             config=dict(workload=f"{a.workload}: {'bivariate' if D == 2 else 'trivariate'} M2, covariates {covs}",
-                        n_customers=n_total, chains=chains, n_mh_steps=20, burnin=burnin, mcmc=mcmc,
+                        n_customers=n_total, chains=chains, n_mh_steps=20, burnin=burnin, mcmc=mcmc_workload,
                         thin=thin, seed=42, draw_sink=sink, parallelism=f"customer-shard x{world}",
                         timed_region="hipGraph replay of fused sweep launches" if not sharded else
                         f"torch.cuda graph replay ({a.graph_chunk} sweeps: sweep + group kernels, RCCL all_gather, "
