@@ -184,6 +184,42 @@ int clv_debug_hyper_variates(uint64_t seed, int32_t chain, uint32_t sweep, doubl
 /* The Philox-mode MH step's fp64 exp (csrc/fastmath.h, |x| <= 700) on n values. */
 int clv_debug_exp(const double* x, int64_t n, double* out);
 
+/* ---- Posterior analysis on device ----
+ * Inputs are level-1 draws [n_draws][n][width] in the reference's layout, chains stacked
+ * (np.vstack of draws["level_1"]); width 4 = (lambda, mu, tau, z), 5 = (+ eta).  The plain
+ * variants take host arrays (uploaded, device = ordinal or -1 for the current one); the
+ * *_sampler variants use the draws a CLV_SINK_FULL sampler holds in HBM after its run. */
+enum {
+  CLV_L1_MEAN_LAMBDA = 0, CLV_L1_LAMBDA_P025, CLV_L1_LAMBDA_P975, CLV_L1_MEAN_MU, CLV_L1_MEAN_MU_CAPPED,
+  CLV_L1_MU_P025, CLV_L1_MU_P975, CLV_L1_MEAN_Z, CLV_L1_MEAN_TAU, CLV_L1_MEAN_ETA, CLV_N_L1_STATS
+};
+/* Posterior predictive future transactions: bivariate/mcmc.py:506-546 (draw_future_transactions)
+ * and, with simulate_spend = 1 (width 5), the lognormal spend totals of trivariate/mcmc.py:660-749.
+ * x_future int64 [n_draws][n]; spend_future float64 [n_draws][n] or NULL. */
+int clv_predict(int32_t device, const double* level1, int64_t n_draws, int64_t n, int32_t width,
+                const double* T_cal, double T_star, uint64_t seed, int32_t simulate_spend, double sigma_s,
+                int64_t* x_future, double* spend_future);
+int clv_predict_sampler(clv_sampler* s, double T_star, uint64_t seed, int32_t simulate_spend,
+                        double sigma_s, int64_t* x_future, double* spend_future);
+/* Weekly tracking curve of bivariate/analysis_abe.py:444-464: for each week t of `times`
+ * (ascending), the mean over draws of the posterior-predictive number of repeat transactions of
+ * the customers active in that week (birth_week < t <= birth_week + tau).  inc_weekly [n_times]. */
+int clv_track(int32_t device, const double* level1, int64_t n_draws, int64_t n, int32_t width,
+              const double* birth_week, const double* times, int32_t n_times, uint64_t seed,
+              double* inc_weekly);
+int clv_track_sampler(clv_sampler* s, const double* birth_week, const double* times, int32_t n_times,
+                      uint64_t seed, double* inc_weekly);
+/* Per-customer posterior statistics (out [n][CLV_N_L1_STATS]): means as numpy's axis-0 mean,
+ * capped-mu mean min(mu, mu_cap) and numpy-'linear' 2.5/97.5 percentiles of lambda and mu —
+ * utils/analysis_bi_helpers.py:15-27 (post_mean_*) and :75-107 (compute_table4). */
+int clv_level1_summary(int32_t device, const double* level1, int64_t n_draws, int64_t n, int32_t width,
+                       double mu_cap, double* out);
+int clv_level1_summary_sampler(clv_sampler* s, double mu_cap, double* out);
+/* Mean over draws of the total log-likelihood incl. -lgamma(x+1) (analysis_bi_helpers.py:52-72). */
+int clv_chain_total_loglik(int32_t device, const double* level1, int64_t n_draws, int64_t n, int32_t width,
+                           const int32_t* x, const double* T_cal, double* mean_total);
+int clv_chain_total_loglik_sampler(clv_sampler* s, double* mean_total);
+
 #ifdef __cplusplus
 }
 #endif

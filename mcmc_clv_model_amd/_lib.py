@@ -108,6 +108,15 @@ def lib() -> ctypes.CDLL:
         "clv_debug_stamps": (c_int32, [sp, POINTER(c_uint64)]),
         "clv_debug_wg_stamps": (c_int32, [sp, POINTER(c_uint64)]),
         "clv_debug_exp": (c_int32, [dp, c_int64, dp]),
+        "clv_predict": (c_int32, [c_int32, dp, c_int64, c_int64, c_int32, dp, c_double, c_uint64, c_int32, c_double,
+                                  POINTER(c_int64), dp]),
+        "clv_predict_sampler": (c_int32, [sp, c_double, c_uint64, c_int32, c_double, POINTER(c_int64), dp]),
+        "clv_track": (c_int32, [c_int32, dp, c_int64, c_int64, c_int32, dp, dp, c_int32, c_uint64, dp]),
+        "clv_track_sampler": (c_int32, [sp, dp, dp, c_int32, c_uint64, dp]),
+        "clv_level1_summary": (c_int32, [c_int32, dp, c_int64, c_int64, c_int32, c_double, dp]),
+        "clv_level1_summary_sampler": (c_int32, [sp, c_double, dp]),
+        "clv_chain_total_loglik": (c_int32, [c_int32, dp, c_int64, c_int64, c_int32, POINTER(c_int32), dp, dp]),
+        "clv_chain_total_loglik_sampler": (c_int32, [sp, dp]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(L, name)
@@ -120,6 +129,11 @@ def lib() -> ctypes.CDLL:
             raise ClvError(f"ctypes mirror of {st.__name__} does not match the C struct; rebuild")
     _lib = L
     return L
+
+
+# Columns of clv_level1_summary() (include/clvmcmc.h CLV_L1_*).
+L1_STATS = ("mean_lambda", "lambda_p025", "lambda_p975", "mean_mu", "mean_mu_capped", "mu_p025", "mu_p975",
+            "mean_z", "mean_tau", "mean_eta")
 
 
 def exported_symbols():

@@ -14,9 +14,10 @@ from __future__ import annotations
 
 from typing import Optional, Sequence
 
+from .analysis import draw_future_transactions  # bi:506-546 (posterior predictive, csrc/analysis.hip)
 from .sampler import build_problem, fit
 
-__all__ = ["mcmc_draw_parameters"]
+__all__ = ["mcmc_draw_parameters", "draw_future_transactions"]
 
 
 def mcmc_draw_parameters(cal_cbs, covariates: Optional[Sequence[str]] = None, mcmc: int = 2500,

@@ -9,6 +9,7 @@
 #include <string>
 #include <vector>
 
+#include "internal.h"
 #include "kernels.h"
 #include "philox.h"
 
@@ -18,67 +19,16 @@ namespace {
 
 thread_local std::string g_err;
 
-int fail(int code, const std::string& msg) {
-  g_err = msg;
-  return code;
-}
-
-#define CLV_HIP(expr)                                                                           \
-  do {                                                                                          \
-    hipError_t e_ = (expr);                                                                     \
-    if (e_ != hipSuccess)                                                                       \
-      return fail(CLV_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_));                 \
-  } while (0)
-
-template <class T>
-hipError_t dalloc(T** p, size_t count) {
-  *p = nullptr;
-  if (count == 0) return hipSuccess;
-  return hipMalloc((void**)p, count * sizeof(T));
-}
-
 constexpr int PRIOR_DOUBLES = 81 + 81 + 27 + 9;  // V, cholV, A0B0, S0B
 constexpr int GRAPH_CHUNK = 64;                  // sweeps per captured graph
 constexpr int TIMING_EVENTS = 256;               // sweep launches timed per harvest
 
 }  // namespace
 
-struct clv_sampler {
-  clv_config cfg{};
-  clv_prior prior{};
-  Geometry g{};
-  bool replay = false;
-  int device = 0;
-  hipStream_t stream = nullptr;
-  hipStream_t own = nullptr;  // stream created by the sampler (destroyed with it)
-  bool own_stream = false;
-
-  int32_t* d_x = nullptr;
-  double *d_tx = nullptr, *d_T = nullptr, *d_cov = nullptr, *d_logs = nullptr;
-  double *d_lam = nullptr, *d_mu = nullptr, *d_hyper = nullptr;
-  double *d_block = nullptr, *d_unit = nullptr;
-  double* d_prior = nullptr;
-  Ctrl* d_ctrl = nullptr;
-  uint32_t* d_arrive = nullptr;     // fused-tail arrival counters: [chain], then [chain][units_per_rank]
-  double* d_hvar = nullptr;         // [chain][HV] precomputed hyper variates
-  unsigned long long* d_stamps = nullptr;  // CLV_STAMPS diagnostic build only
-  double *d_level1 = nullptr, *d_level2 = nullptr, *d_loglik = nullptr, *d_sums = nullptr;
-  double* d_tape = nullptr;
-  double* d_bs = nullptr;  // staging for set_hyper
-  int64_t tape_sweeps = 0;
-
-  bool pending_init_hyper = false;  // bivariate: the draw for sweep 1 is still due
-  int64_t sweeps_done = 0;
-
-  hipGraphExec_t graph_exec = nullptr;
-  int graph_sweeps = 0;
-
-  bool timing = false;
-  std::vector<hipEvent_t> ev;  // 4 per slot: sweep start/end, hyper start/end
-  int ev_used = 0;
-  double t_sweep_ms = 0.0, t_hyper_ms = 0.0;
-  int64_t n_sweep_timed = 0, n_hyper_timed = 0;
-};
+int clv::fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
 
 namespace {
 

@@ -263,6 +263,36 @@ class HipSampler:
         hyp = np.ascontiguousarray(hyp, dtype=np.float64)
         check(self._L.clv_set_state(self.h, dptr(lam), dptr(mu), dptr(hyp), int(sweeps_done)))
 
+    # ---- posterior analysis on the draws this sampler holds in HBM (draw_sink="full", run done)
+    def predict(self, T_star: float = 39.0, seed: Optional[int] = None, simulate_spend: bool = False,
+                sigma_s: float = 0.5):
+        """clv_predict_sampler: analysis.draw_future_transactions without the host round trip."""
+        nd = self.chains * self.n_draws
+        x = np.empty((nd, self.n), np.int64)
+        spend = np.empty((nd, self.n), np.float64) if simulate_spend else None
+        check(self._L.clv_predict_sampler(self.h, float(T_star), resolve_seed(seed), 1 if simulate_spend else 0,
+                                          float(sigma_s), x.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                          dptr(spend)))
+        return (x, spend) if simulate_spend else x
+
+    def level1_summary(self, mu_cap: float = 0.05) -> np.ndarray:
+        """clv_level1_summary_sampler: [n][len(_lib.L1_STATS)] per-customer statistics."""
+        out = np.empty((self.n, len(_lib.L1_STATS)), np.float64)
+        check(self._L.clv_level1_summary_sampler(self.h, float(mu_cap), dptr(out)))
+        return out
+
+    def chain_total_loglik(self) -> float:
+        out = ctypes.c_double()
+        check(self._L.clv_chain_total_loglik_sampler(self.h, ctypes.byref(out)))
+        return float(out.value)
+
+    def track(self, birth_week, times, seed: Optional[int] = 0) -> np.ndarray:
+        b = np.ascontiguousarray(np.asarray(birth_week, dtype=np.float64))
+        t = np.ascontiguousarray(np.asarray(times, dtype=np.float64))
+        out = np.empty(t.shape[0], np.float64)
+        check(self._L.clv_track_sampler(self.h, dptr(b), dptr(t), t.shape[0], resolve_seed(seed), dptr(out)))
+        return out
+
     def set_timing(self, enable: bool) -> None:
         check(self._L.clv_set_timing(self.h, 1 if enable else 0))
 

@@ -8,9 +8,10 @@ from __future__ import annotations
 
 from typing import Optional, Sequence
 
+from .analysis import draw_future_transactions_rfm_m as draw_future_transactions  # tri:660-749
 from .sampler import build_problem, fit
 
-__all__ = ["mcmc_draw_parameters_rfm_m"]
+__all__ = ["mcmc_draw_parameters_rfm_m", "draw_future_transactions"]
 
 
 def mcmc_draw_parameters_rfm_m(cal_cbs, covariates: Optional[Sequence[str]] = None, mcmc: int = 2500,

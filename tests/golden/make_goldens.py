@@ -14,6 +14,9 @@ Fixtures written:
   envelope_*.npz             G3: per-customer posterior summaries over M independent reference chains
   published_table3.json      abe_replication.xlsx "Table 3" (published loose pins)
   oracle_pin.json            the bitwise oracle-vs-reference checks that passed
+  analysis_abe400.npz        row f: the reference's analysis helpers (draw_future_transactions bi/tri,
+                             post_mean_*, chain_total_loglik, compute_table4) on fixed draws
+  analysis_pin.json          the oracle/analysis_cpu.py-vs-reference checks that passed
 
 Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py [--skip-envelope]
 """
@@ -377,6 +380,53 @@ def write_published():
     print("published sheets", list(sheets))
 
 
+# ---------------------------------------------------------------------------------------------
+def write_analysis(rbi, rtri):
+    """Row f fixtures: the reference's analysis helpers on fixed draws (bitwise-pinned oracle)."""
+    sys.path.insert(0, REF)
+    from src.models.utils import analysis_bi_helpers as rh  # noqa: E402
+    from oracle import analysis_cpu as oan  # noqa: E402
+    df = prepare(load_cbs("abe")).iloc[:400].copy()
+    bi = rbi.mcmc_draw_parameters(df, [], mcmc=60, burnin=40, thin=2, chains=2, seed=5, trace=0)
+    tri = rtri.mcmc_draw_parameters_rfm_m(df, [], mcmc=40, burnin=20, thin=2, chains=2, seed=6, trace=0)
+    xs_bi = rbi.draw_future_transactions(df, bi, T_star=39.0, seed=42)
+    xs_tri, sp_tri = rtri.draw_future_transactions(df, tri, T_star=39.0, seed=43)
+    checks = dict(
+        xstar_bi=bitwise_equal(xs_bi, oan.draw_future_transactions_bi(df, bi, 39.0, seed=42)),
+        xstar_tri=all(bitwise_equal(a, b) for a, b in zip((xs_tri, sp_tri),
+                                                         oan.draw_future_transactions_tri(df, tri, 39.0, seed=43))),
+        post_mean_lambdas=bitwise_equal(rh.post_mean_lambdas(bi), oan.post_mean_lambdas(bi)),
+        post_mean_mus=bitwise_equal(rh.post_mean_mus(bi), oan.post_mean_mus(bi)),
+        chain_total_loglik=bitwise_equal(rh.chain_total_loglik(bi["level_1"], df),
+                                         oan.chain_total_loglik(bi["level_1"], df)),
+    )
+    t4 = rh.compute_table4(bi, xs_bi)
+    st = oan.table4_stats(bi)
+    # the reference's Table 4 summary rows (Ave/Min/Max) from the oracle's per-customer columns
+    checks["table4_ave_row"] = bool(np.isclose(float(t4.loc["Ave", "Mean(λ)"]), round(st["mean_lambda"].mean(), 3)))
+    print("analysis pin", checks)
+    if not all(checks.values()):
+        raise SystemExit("analysis oracle differs from the reference; refusing to write fixtures")
+    elog = pd.read_csv(os.path.join(REF, "data", "raw", "cdnow_abeElog.csv"), parse_dates=["date"])
+    first = elog["date"].min()
+    elog["week"] = ((elog["date"] - first) // pd.Timedelta("7D")).astype(int) + 1
+    cust = pd.read_csv(os.path.join(REF, "data", "processed", "cdnow_abeCBS.csv"))["cust"].iloc[:400]
+    birth = elog.groupby("cust")["week"].min().reindex(cust).to_numpy(np.float64)
+    times = np.arange(1, int(elog["week"].max()) + 1, dtype=np.float64)
+    np.savez_compressed(os.path.join(HERE, "analysis_abe400.npz"),
+                        x=df["x"].to_numpy(np.int64), t_x=df["t_x"].to_numpy(), T_cal=df["T_cal"].to_numpy(),
+                        bi_level1=np.stack(bi["level_1"]), tri_level1=np.stack(tri["level_1"]),
+                        xstar_bi=xs_bi, xstar_tri=xs_tri, spend_tri=sp_tri,
+                        post_mean_lambdas=rh.post_mean_lambdas(bi), post_mean_mus=rh.post_mean_mus(bi),
+                        chain_total_loglik=rh.chain_total_loglik(bi["level_1"], df),
+                        table4=t4.to_numpy(dtype=object).astype(str), table4_index=np.array(t4.index.astype(str).tolist(), dtype=str),
+                        table4_columns=np.array(t4.columns, dtype=str),
+                        birth_week=birth, times=times,
+                        tracking_ref=oan.weekly_tracking(bi, birth, times), **{f"t4_{k}": v for k, v in st.items()})
+    with open(os.path.join(HERE, "analysis_pin.json"), "w") as f:
+        json.dump(dict(checks=checks, note="reference helpers vs oracle/analysis_cpu.py on the same draws"), f, indent=1)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-envelope", action="store_true")
@@ -386,7 +436,7 @@ def main():
     only = set(a.only.split(",")) if a.only else None
     steps = [("pin", lambda: pin_oracle(rbi, rtri)), ("data", write_data), ("philox", write_philox_kat),
              ("formulas", lambda: write_formulas(rbi, rtri)), ("replay", lambda: write_replay(rbi, rtri)),
-             ("published", write_published)]
+             ("published", write_published), ("analysis", lambda: write_analysis(rbi, rtri))]
     if not a.skip_envelope:
         steps.append(("envelope", write_envelope))
     for name, fn in steps:
