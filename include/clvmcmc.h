@@ -220,6 +220,28 @@ int clv_chain_total_loglik(int32_t device, const double* level1, int64_t n_draws
                            const int32_t* x, const double* T_cal, double* mean_total);
 int clv_chain_total_loglik_sampler(clv_sampler* s, double* mean_total);
 
+/* ---- Data preparation on device ----
+ * Event log -> CBS (utils/elog2cbs2param.py:33-94): events (cust, date in ns since the epoch,
+ * sales or NULL = 1) -> one row per customer with calibration events, sorted by cust.  Output
+ * buffers hold n_events rows (upper bound); *n_customers rows are written.  Hold-out columns
+ * (T_star, x_star, sales_star) are meaningful when T_cal_ns < T_tot_ns. */
+int clv_elog2cbs(int32_t device, int64_t n_events, const int64_t* cust, const int64_t* date_ns, const double* sales,
+                 int64_t unit_ns, int64_t T_cal_ns, int64_t T_tot_ns, int64_t* n_customers, int64_t* cust_out,
+                 int64_t* x, double* t_x, double* litt, double* sales_out, double* sales_x, int64_t* first_ns,
+                 double* T_cal, double* T_star, int64_t* x_star, double* sales_star);
+/* Synthetic Abe (2009) data (bivariate/mcmc.py:95-187): covariates [1, U(-1,1)...] (or the
+ * caller's [n][K] incl. intercept), theta = exp(X beta + MVN(0, gamma)), tau ~ Exp(mu), purchases
+ * as a Poisson process until min(T_cal + max T_star, tau); CBS of bi:75-89 and hold-out counts
+ * x_star[n_star][n].  beta K x 2 row-major, gamma 2 x 2, T_cal[n].  n_events = elog rows per
+ * customer; with elog_offsets (exclusive prefix sum of n_events from a first call) a second call
+ * also writes the elog (cust 1-based, t). */
+int clv_generate_pareto_abe(int32_t device, int64_t n, int32_t K, const double* beta, const double* gamma,
+                            const double* covars, const double* T_cal, int32_t n_star, const double* T_star,
+                            uint64_t seed, int64_t* x, double* t_x, double* lambda_true, double* mu_true,
+                            double* tau_true, uint8_t* alive_true, int64_t* x_star, double* covars_out,
+                            int64_t* n_events, const int64_t* elog_offsets, int64_t elog_rows, int64_t* elog_cust,
+                            double* elog_t);
+
 #ifdef __cplusplus
 }
 #endif

@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from ctypes import POINTER, c_char_p, c_double, c_float, c_int32, c_int64, c_uint32, c_uint64, c_void_p
+from ctypes import c_uint8, POINTER, c_char_p, c_double, c_float, c_int32, c_int64, c_uint32, c_uint64, c_void_p
 
 try:  # share torch's HIP runtime when torch is present (see module docstring)
     import torch  # noqa: F401
@@ -117,6 +117,12 @@ def lib() -> ctypes.CDLL:
         "clv_level1_summary_sampler": (c_int32, [sp, c_double, dp]),
         "clv_chain_total_loglik": (c_int32, [c_int32, dp, c_int64, c_int64, c_int32, POINTER(c_int32), dp, dp]),
         "clv_chain_total_loglik_sampler": (c_int32, [sp, dp]),
+        "clv_elog2cbs": (c_int32, [c_int32, c_int64, POINTER(c_int64), POINTER(c_int64), dp, c_int64, c_int64, c_int64,
+                                   POINTER(c_int64), POINTER(c_int64), POINTER(c_int64), dp, dp, dp, dp,
+                                   POINTER(c_int64), dp, dp, POINTER(c_int64), dp]),
+        "clv_generate_pareto_abe": (c_int32, [c_int32, c_int64, c_int32, dp, dp, dp, dp, c_int32, dp, c_uint64,
+                                              POINTER(c_int64), dp, dp, dp, dp, POINTER(c_uint8), POINTER(c_int64), dp,
+                                              POINTER(c_int64), POINTER(c_int64), c_int64, POINTER(c_int64), dp]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(L, name)

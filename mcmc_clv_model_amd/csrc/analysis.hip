@@ -277,13 +277,6 @@ __global__ __launch_bounds__(256) void loglik_kernel(const double* level1, int64
 // ---------------------------------------------------------------------------------------------
 // Host helpers
 // ---------------------------------------------------------------------------------------------
-struct DevBuf {
-  void* p = nullptr;
-  ~DevBuf() {
-    if (p) (void)hipFree(p);
-  }
-};
-
 int check_l1(int64_t n_draws, int64_t n, int32_t width) {
   if (n_draws < 1 || n < 1 || (width != 4 && width != 5)) return fail(CLV_EINVAL, "bad level-1 shape");
   if (n > 0xffffffffLL || n_draws > 0xffffffffLL) return fail(CLV_EINVAL, "level-1 shape exceeds the 32-bit Philox counter words");
@@ -427,17 +420,6 @@ int sampler_l1(clv_sampler* s, const double** l1, int64_t* n_draws, int32_t* wid
   *width = s->g.D + 2;
   return check_l1(*n_draws, s->g.n, *width);
 }
-
-struct DeviceScope {
-  int prev = -1;
-  explicit DeviceScope(int dev) {
-    (void)hipGetDevice(&prev);
-    if (dev >= 0) (void)hipSetDevice(dev);
-  }
-  ~DeviceScope() {
-    if (prev >= 0) (void)hipSetDevice(prev);
-  }
-};
 
 }  // namespace
 

@@ -20,6 +20,33 @@ hipError_t dalloc(T** p, size_t count) {
   return hipMalloc((void**)p, count * sizeof(T));
 }
 
+// Owning device allocation (freed on scope exit) and a scoped device switch, for the host-side
+// orchestration of the analysis / data-preparation entry points.
+struct DevBuf {
+  void* p = nullptr;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+  template <class T>
+  T* as() const {
+    return (T*)p;
+  }
+};
+
+struct DeviceScope {
+  int prev = -1;
+  explicit DeviceScope(int dev) {
+    (void)hipGetDevice(&prev);
+    if (dev >= 0) (void)hipSetDevice(dev);
+  }
+  ~DeviceScope() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
 }  // namespace clv
 
 #define CLV_HIP(expr)                                                                           \

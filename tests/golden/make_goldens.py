@@ -17,6 +17,9 @@ Fixtures written:
   analysis_abe400.npz        row f: the reference's analysis helpers (draw_future_transactions bi/tri,
                              post_mean_*, chain_total_loglik, compute_table4) on fixed draws
   analysis_pin.json          the oracle/analysis_cpu.py-vs-reference checks that passed
+  elog_abe.npz               row f4: cdnow_abeElog.csv and the reference elog2cbs outputs (W with
+                             hold-out, D without, W without a sales column)
+  generator_bi.npz           row f4: a 20,000-customer sample of the reference's generate_pareto_abe
 
 Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py [--skip-envelope]
 """
@@ -427,6 +430,37 @@ def write_analysis(rbi, rtri):
         json.dump(dict(checks=checks, note="reference helpers vs oracle/analysis_cpu.py on the same draws"), f, indent=1)
 
 
+# ---------------------------------------------------------------------------------------------
+def write_dataprep(rbi):
+    """Row f4 fixtures: the reference's elog2cbs (utils/elog2cbs2param.py) on the CDNOW 1/10 event
+    log, and a sample of its synthetic generator (bi:95-187)."""
+    sys.path.insert(0, REF)
+    from src.models.utils.elog2cbs2param import elog2cbs as ref_elog2cbs  # noqa: E402
+    elog = pd.read_csv(os.path.join(REF, "data", "raw", "cdnow_abeElog.csv"))
+    elog["date"] = pd.to_datetime(elog["date"])
+    out = {}
+    cases = {"hold": dict(units="W", T_cal="1997-09-30", T_tot="1998-06-30"),
+             "nohold": dict(units="D", T_cal=None, T_tot=None)}
+    for tag, kw in cases.items():
+        cbs = ref_elog2cbs(elog, **kw)
+        for c in cbs.columns:
+            v = cbs[c]
+            out[f"{tag}_{c}"] = v.to_numpy(dtype="datetime64[ns]").view(np.int64) if c == "first" else v.to_numpy()
+    nos = ref_elog2cbs(elog[["cust", "date"]], units="W", T_cal="1997-09-30", T_tot="1998-06-30")
+    for c in ("x", "sales", "sales_x", "x_star", "sales_star"):
+        out[f"nosales_{c}"] = nos[c].to_numpy()
+    np.savez_compressed(os.path.join(HERE, "elog_abe.npz"), cust=elog["cust"].to_numpy(np.int64),
+                        date_ns=elog["date"].to_numpy(dtype="datetime64[ns]").view(np.int64),
+                        sales=elog["sales"].to_numpy(np.float64), **out)
+    beta = np.array([[0.18, -2.5], [0.3, -0.2]])
+    gamma = np.array([[0.05, 0.1], [0.1, 0.2]])
+    cbs, el = rbi.generate_pareto_abe(20000, 32.0, [20.0, 32.0], beta, gamma, seed=2025)
+    np.savez_compressed(os.path.join(HERE, "generator_bi.npz"), beta=beta, gamma=gamma, T_cal_in=32.0,
+                        T_star=np.array([20.0, 32.0]), n_elog=len(el),
+                        **{c: cbs[c].to_numpy(np.float64) for c in cbs.columns})
+    print("dataprep", {k: v.shape for k, v in out.items() if k.endswith("_x")}, len(cbs), len(el))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-envelope", action="store_true")
@@ -436,7 +470,8 @@ def main():
     only = set(a.only.split(",")) if a.only else None
     steps = [("pin", lambda: pin_oracle(rbi, rtri)), ("data", write_data), ("philox", write_philox_kat),
              ("formulas", lambda: write_formulas(rbi, rtri)), ("replay", lambda: write_replay(rbi, rtri)),
-             ("published", write_published), ("analysis", lambda: write_analysis(rbi, rtri))]
+             ("published", write_published), ("analysis", lambda: write_analysis(rbi, rtri)),
+             ("dataprep", lambda: write_dataprep(rbi))]
     if not a.skip_envelope:
         steps.append(("envelope", write_envelope))
     for name, fn in steps:
