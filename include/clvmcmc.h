@@ -175,8 +175,9 @@ int clv_debug_level2(int32_t D, int32_t K, const clv_prior* prior, const double*
 /* Diagnostic build only (make STAMPS=1 -> libclvmcmc_stamps.so): per-sweep s_memrealtime stamps
  * [1024][8] (slot = sweep % 1024); CLV_ESTATE in the shipped library. */
 int clv_debug_stamps(clv_sampler* s, uint64_t* out);
-/* Diagnostic build only: per workgroup of the latest sweep launch [chain][block][4] =
- * (start, end of customer work, HW_ID, XCC_ID); CLV_ESTATE in the shipped library. */
+/* Diagnostic build only: per workgroup of the latest sweep launch [chain][block][8] = (start,
+ * end of customer work (s_memrealtime), HW_ID, XCC_ID, s_memtime at start / MH start / MH end /
+ * end of customer work); CLV_ESTATE in the shipped library. */
 int clv_debug_wg_stamps(clv_sampler* s, uint64_t* out);
 /* Philox-mode chi-square and normal draws of the hyper stream (n of each). */
 int clv_debug_hyper_variates(uint64_t seed, int32_t chain, uint32_t sweep, double df, int64_t n,

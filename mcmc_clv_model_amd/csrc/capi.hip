@@ -314,7 +314,7 @@ int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* pri
   CLV_HIPC(dalloc(&s->d_hvar, C * HV));
 #ifdef CLV_STAMPS
   {
-    std::vector<unsigned long long> st(1024 * 8 + 4 * (size_t)C * std::max(nb_local, 1), 0ull);
+    std::vector<unsigned long long> st(1024 * 8 + 12 * (size_t)C * std::max(nb_local, 1), 0ull);
     for (int i = 0; i < 1024; ++i) st[i * 8 + 0] = st[i * 8 + 4] = ~0ull;
     CLV_HIPC(dalloc(&s->d_stamps, st.size()));
     CLV_HIPC(hipMemcpy(s->d_stamps, st.data(), st.size() * sizeof(unsigned long long), hipMemcpyHostToDevice));
@@ -664,7 +664,7 @@ int clv_debug_wg_stamps(clv_sampler* s, uint64_t* out) {
   if (!s || !out) return fail(CLV_EINVAL, "null argument");
   if (!s->d_stamps) return fail(CLV_ESTATE, "library not built with CLV_STAMPS (make STAMPS=1)");
   CLV_HIP(hipStreamSynchronize(s->stream));
-  CLV_HIP(hipMemcpy(out, s->d_stamps + 1024 * 8, sizeof(uint64_t) * 4 * s->g.n_chains * s->g.nb_local,
+  CLV_HIP(hipMemcpy(out, s->d_stamps + 1024 * 8, sizeof(uint64_t) * 12 * s->g.n_chains * s->g.nb_local,
                     hipMemcpyDeviceToHost));
   return CLV_OK;
 }

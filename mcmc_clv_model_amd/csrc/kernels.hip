@@ -156,15 +156,18 @@ __device__ __forceinline__ void stamp(unsigned long long* st, int64_t s, int k, 
   else __hip_atomic_fetch_max(p, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 #define CLV_STAMP(st, s, k, is_min) stamp(st, s, k, is_min)
-// per-workgroup record of the latest launch after the 1024 x 8 sweep stamps:
-// [start, end of customer work, HW_ID, XCC_ID] (placement diagnostics)
+// per-workgroup record of the latest launch after the 1024 x 8 sweep stamps (wave 0, lane 0):
+// [0] s_memrealtime start [1] s_memrealtime end of customer work [2] HW_ID [3] XCC_ID
+// [4] s_memtime start [5] s_memtime MH start [6] s_memtime MH end [7] s_memtime end of customer work
+// [8] s_memtime after the workgroup barrier [9] s_memtime after draw_z / draw_tau
 __device__ __forceinline__ void wg_stamp(unsigned long long* st, int64_t wg, int k) {
   if (!st) return;
   unsigned long long v;
   if (k < 2) v = __builtin_amdgcn_s_memrealtime();
   else if (k == 2) v = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));   // HW_REG_HW_ID
-  else v = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11));             // HW_REG_XCC_ID
-  st[1024 * 8 + wg * 4 + k] = v;
+  else if (k == 3) v = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11));  // HW_REG_XCC_ID
+  else v = __builtin_amdgcn_s_memtime();
+  st[1024 * 8 + wg * 12 + k] = v;
 }
 #define CLV_WG_STAMP(st, wg, k) wg_stamp(st, wg, k)
 #else
@@ -539,6 +542,7 @@ struct Cust {
   bool active;
   double xr[K];       // [1, covariates]
   double tx, T, xm;
+  int32_t xi;         // x as loaded (converted in cust_prepare, so the load is not waited for early)
   double lam, mu, eta, tau;
   bool z;
   double ll, lm, cur; // MH state (log scale) and its log posterior
@@ -561,7 +565,7 @@ __device__ __forceinline__ void cust_load(Cust<D, K>& u, const SweepArgs& a, int
   const int64_t ci = (int64_t)c * g.n + i;
   u.lam = a.lam[ci];
   u.mu = a.mu[ci];
-  u.xm = (double)a.x[i];
+  u.xi = a.x[i];
   u.gi = (uint32_t)(g.shard_begin + i);
 }
 
@@ -573,6 +577,9 @@ __device__ __forceinline__ void cust_prepare(Cust<D, K>& u, const SweepArgs& a, 
   const int64_t i = u.i;
   const double lam = u.lam, mu = u.mu;
   const double tx = u.tx, T = u.T;
+  int32_t xi = u.xi;
+  asm volatile("" : "+v"(xi));  // keeps the int->double conversion (and its load wait) here
+  u.xm = (double)xi;
 
   // ---- draw_z (bi:193-200)
   // Replay: u_z and the per-customer tau variate (standard exponential if alive, uniform if
@@ -772,9 +779,18 @@ __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
   const Geometry& g = a.g;
   const int c = blockIdx.y;
   const int b = blockIdx.x;
-  // the sweep index is uniform: readfirstlane keeps it (and the Philox words derived from it) in
-  // scalar registers — a vector atomic load alone would make it look divergent to the compiler
-  const int64_t s = a.init ? 0 : uniform_i64(__hip_atomic_load(&a.ctrl->cur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + 1;
+  // The customer's loads go out first, so that their latency, the exp table's and the sweep
+  // index's overlap (one memory round trip before compute instead of several).
+  Cust<D, K> cu;
+  {
+    const int64_t i = (int64_t)b * BLOCK + threadIdx.x;
+    cu.active = i < g.n;
+    cu.i = cu.active ? i : (g.n > 0 ? g.n - 1 : 0);
+  }
+  if (!a.init && g.n > 0) cust_load(cu, a, c);  // inactive lanes load a clamped valid row
+  // The sweep index: a scalar load of the uniform counter (written by the previous launch's tail;
+  // this launch's tail overwrites it only after every workgroup has arrived, i.e. read it).
+  const int64_t s = a.init ? 0 : a.ctrl->cur + 1;
   const bool stored = !a.init && is_stored(s, g);
 
   double acc[NS];
@@ -786,13 +802,7 @@ __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
     CLV_WG_STAMP(a.stamps, (int64_t)c * g.nb_local + b, 0);
     CLV_WG_STAMP(a.stamps, (int64_t)c * g.nb_local + b, 2);
     CLV_WG_STAMP(a.stamps, (int64_t)c * g.nb_local + b, 3);
-  }
-
-  Cust<D, K> cu;
-  {
-    const int64_t i = (int64_t)b * BLOCK + threadIdx.x;
-    cu.active = i < g.n;
-    cu.i = cu.active ? i : (g.n > 0 ? g.n - 1 : 0);
+    CLV_WG_STAMP(a.stamps, (int64_t)c * g.nb_local + b, 4);
   }
 
   if (a.init) {
@@ -823,9 +833,9 @@ __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
         for (int r = p; r < D; ++r) acc[t++] += Y[p] * Y[r];
     }
   }
-  if (!a.init && g.n > 0) cust_load(cu, a, c);  // inactive lanes load a clamped valid row
   if (!REPLAY) exp_tab[threadIdx.x] = tab_v;
   __syncthreads();
+  if (threadIdx.x == 0 && !a.init) CLV_WG_STAMP(a.stamps, (int64_t)c * g.nb_local + b, 8);
 
   // ---- the next level-2 draw's Philox variates (independent of the statistics): computed by
   // the last wavefront of the chain's last workgroup — the partially filled one — so the draw's
@@ -862,6 +872,7 @@ __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
       chain_key(a.r.seed, (int64_t)a.r.chain_first + c, &k0, &k1);
     }
     cust_prepare<D, K, REPLAY>(cu, a, c, s, H, k0, k1, tape, exp_tab);
+    if (threadIdx.x == 0) CLV_WG_STAMP(a.stamps, (int64_t)c * g.nb_local + b, 9);
     const double s00 = H[H_S00];
     const double s11 = H[H_S11];
     if constexpr (REPLAY) {
@@ -889,6 +900,7 @@ __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
       float tl[MC], tm[MC], lu[MC];
       const SlotPhilox ph(k0, k1, cu.gi, (uint32_t)s);
       const int n_chunks = (g.S + MC - 1) / MC;
+      if (threadIdx.x == 0) CLV_WG_STAMP(a.stamps, (int64_t)c * g.nb_local + b, 5);
       if (n_chunks > 0) mh_chunk_variates(ph, 0u, tl, tm, lu);
       for (int ch = 0; ch < n_chunks; ++ch) {
         float ntl[MC], ntm[MC], nlu[MC];
@@ -904,6 +916,7 @@ __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
         }
       }
     }
+    if (threadIdx.x == 0) CLV_WG_STAMP(a.stamps, (int64_t)c * g.nb_local + b, 6);
     cust_finish<D, K, REPLAY, NS>(cu, a, c, s, stored, H, k0, k1, tape, exp_tab, acc);
   }
 
@@ -963,6 +976,7 @@ __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
       CLV_STAMP(a.stamps, s, 1, false);
       CLV_STAMP(a.stamps, s, 4, true);
       CLV_WG_STAMP(a.stamps, (int64_t)c * g.nb_local + b, 1);
+      CLV_WG_STAMP(a.stamps, (int64_t)c * g.nb_local + b, 7);
       const uint32_t n_arrivals = (uint32_t)((g.nb_local + bpu - 1) / bpu);  // units in the launch
       const uint32_t old = __hip_atomic_fetch_add(a.chain_arrive + c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const uint32_t last = old == n_arrivals - 1 ? 1u : 0u;

@@ -45,9 +45,9 @@ def main(workload="c2", sweeps=1500, chains=None):
     print(f"    tail: record + counters               {us(st[:, 3] - st[:, 7]):8.2f} us")
     # placement of the latest launch's workgroups: per CU (XCC, SE, CU) count and durations
     nb = -(-s.n // 256)
-    wg = np.zeros(s.chains * nb * 4, np.uint64)
+    wg = np.zeros(s.chains * nb * 12, np.uint64)
     assert s._L.clv_debug_wg_stamps(s.h, wg.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))) == 0
-    wg = wg.reshape(-1, 4).astype(np.int64)
+    wg = wg.reshape(-1, 12).astype(np.int64)
     hw, xcc = wg[:, 2], wg[:, 3] & 0xF
     cu, se = (hw >> 8) & 0xF, (hw >> 13) & 0x7
     key = xcc * 1000 + se * 100 + cu
@@ -59,6 +59,20 @@ def main(workload="c2", sweeps=1500, chains=None):
     for k in sorted(set(per_wg_cnt.tolist())):
         d = dur[per_wg_cnt == k]
         print(f"    CUs with {k} WG(s): WG customer-phase duration median {np.median(d):7.2f} us, max {d.max():7.2f} us")
+    ok2 = (wg[:, 7] > wg[:, 4]) & (wg[:, 1] > wg[:, 0])
+    clk = (wg[ok2, 7] - wg[ok2, 4]) / ((wg[ok2, 1] - wg[ok2, 0]) * 1e-8) / 1e9
+    mh = wg[ok2, 6] - wg[ok2, 5]
+    pre = wg[ok2, 5] - wg[ok2, 4]
+    post = wg[ok2, 7] - wg[ok2, 6]
+    pc = per_wg_cnt[ok2]
+    print(f"  shader clock (s_memtime / s_memrealtime): median {np.median(clk):.2f} GHz")
+    for k in sorted(set(pc.tolist())):
+        sel = pc == k
+        bar = (wg[ok2, 8] - wg[ok2, 4])[sel]
+        zt = (wg[ok2, 9] - wg[ok2, 8])[sel]
+        print(f"    CUs with {k} WG(s): wave-0 cycles  start->barrier {np.median(bar):7.0f}  z/tau {np.median(zt):7.0f}"
+              f"  ->MH {np.median(pre[sel] - bar - zt):6.0f}  MH {np.median(mh[sel]):8.0f}"
+              f"  finish+reduce {np.median(post[sel]):8.0f}")
     print("  WGs per XCC:", {int(k): int(v) for k, v in zip(*np.unique(xcc, return_counts=True))})
     s.close()
 
