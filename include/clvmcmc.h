@@ -135,6 +135,10 @@ int clv_partials(clv_sampler* s, double** device_ptr, int64_t* n_doubles, int32_
 int clv_copy_partials(clv_sampler* s, void* dst_device_ptr);
 int clv_synchronize(clv_sampler* s);
 int64_t clv_sweeps_done(const clv_sampler* s);
+/* How clv_run launches: out[4] = (persistent 0/1, persistent-kernel workgroups per CU, CUs,
+ * workgroups per sweep).  Persistent = one launch for all of a clv_run's sweeps, chosen at create
+ * when world_size == 1, Philox mode, every workgroup fits at once, and CLV_PERSISTENT != "0". */
+int clv_launch_info(const clv_sampler* s, int64_t* out);
 /* Launch on another stream from now on (e.g. a stream under hipGraph capture by the caller,
  * who then replays the captured sweeps), and adjust the host's sweep count by n (+chunk per
  * replay; -chunk after a capture, which records launches without executing them). */
@@ -175,9 +179,11 @@ int clv_debug_level2(int32_t D, int32_t K, const clv_prior* prior, const double*
 /* Diagnostic build only (make STAMPS=1 -> libclvmcmc_stamps.so): per-sweep s_memrealtime stamps
  * [1024][8] (slot = sweep % 1024); CLV_ESTATE in the shipped library. */
 int clv_debug_stamps(clv_sampler* s, uint64_t* out);
-/* Diagnostic build only: per workgroup of the latest sweep launch [chain][block][8] = (start,
- * end of customer work (s_memrealtime), HW_ID, XCC_ID, s_memtime at start / MH start / MH end /
- * end of customer work); CLV_ESTATE in the shipped library. */
+/* Diagnostic build only: per workgroup of the latest sweep launch, [chain * n_blocks + 1 per chain]
+ * records of 12 u64 (sweep kernel: start / end of customer work (s_memrealtime), HW_ID, XCC_ID,
+ * s_memtime phase stamps; persistent kernel: s_memrealtime phase stamps of one sweep, see
+ * kernels.hip CLV_P_STAMP); out must hold 12 * n_chains * (n_blocks + 1) values; CLV_ESTATE in
+ * the shipped library. */
 int clv_debug_wg_stamps(clv_sampler* s, uint64_t* out);
 /* Philox-mode chi-square and normal draws of the hyper stream (n of each). */
 int clv_debug_hyper_variates(uint64_t seed, int32_t chain, uint32_t sweep, double df, int64_t n,

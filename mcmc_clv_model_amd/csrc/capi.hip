@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -60,6 +61,8 @@ SweepArgs sweep_args(clv_sampler* s, int init, int fuse = 0) {
   a.fuse = fuse;
   a.chain_arrive = s->d_arrive;
   a.unit_arrive = s->d_arrive + s->g.n_chains;
+  a.ctrl_rw = s->d_ctrl;
+  a.hyp2 = s->d_hyp2;
   a.unitpart = s->d_unit;
   a.hvar_out = s->d_hvar;
   a.stamps = s->d_stamps;
@@ -134,9 +137,8 @@ int harvest_timing(clv_sampler* s) {
   for (int k = 0; k < s->ev_used; ++k) {
     float ms = 0.f;
     CLV_HIP(hipEventElapsedTime(&ms, s->ev[4 * k], s->ev[4 * k + 1]));
-    s->t_sweep_ms += ms;
-    s->n_sweep_timed++;
-    (void)0;  // fused: the level-2 draw is inside the timed sweep launch
+    s->t_sweep_ms += ms;  // fused: the level-2 draw is inside the timed launch
+    s->n_sweep_timed += s->ev_sweeps.empty() ? 1 : s->ev_sweeps[k];  // persistent: many sweeps
   }
   s->ev_used = 0;
   return CLV_OK;
@@ -312,9 +314,21 @@ int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* pri
   CLV_HIPC(dalloc(&s->d_ctrl, 1));
   CLV_HIPC(dalloc(&s->d_arrive, C + C * (int64_t)g.units_per_rank));  // chain, then unit counters
   CLV_HIPC(dalloc(&s->d_hvar, C * HV));
+  CLV_HIPC(dalloc(&s->d_hyp2, 2 * C * HS));
+  // Persistent sweeps (one launch runs many sweeps) when every workgroup of the grid can be
+  // resident at once — the chain hand-off spins on the other workgroups (CLV_PERSISTENT=0 opts out)
+  if (!s->replay && cfg->world_size == 1 && nb_local > 0 && bpu == 1 && nb_local <= 2 * BLOCK) {
+    const char* env = std::getenv("CLV_PERSISTENT");
+    hipDeviceProp_t prop{};
+    if (persist_occupancy(g.D, g.K, &s->persist_bpc) == hipSuccess &&
+        hipGetDeviceProperties(&prop, s->device) == hipSuccess)
+      s->n_cu = prop.multiProcessorCount;
+    if ((!env || std::string(env) != "0") && (int64_t)s->persist_bpc * s->n_cu >= (int64_t)(nb_local + 1) * C)
+      s->persistent = true;
+  }
 #ifdef CLV_STAMPS
   {
-    std::vector<unsigned long long> st(1024 * 8 + 12 * (size_t)C * std::max(nb_local, 1), 0ull);
+    std::vector<unsigned long long> st(1024 * 8 + 12 * (size_t)C * (std::max(nb_local, 1) + 1), 0ull);
     for (int i = 0; i < 1024; ++i) st[i * 8 + 0] = st[i * 8 + 4] = ~0ull;
     CLV_HIPC(dalloc(&s->d_stamps, st.size()));
     CLV_HIPC(hipMemcpy(s->d_stamps, st.data(), st.size() * sizeof(unsigned long long), hipMemcpyHostToDevice));
@@ -405,6 +419,7 @@ void clv_destroy(clv_sampler* s) {
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (s->d_unit && s->d_unit != s->d_block) (void)hipFree(s->d_unit);
+  if (s->d_hyp2) (void)hipFree(s->d_hyp2);
   if (s->own_stream && s->own) (void)hipStreamDestroy(s->own);
   delete s;
 }
@@ -489,6 +504,15 @@ int clv_synchronize(clv_sampler* s) {
 
 int64_t clv_sweeps_done(const clv_sampler* s) { return s ? s->sweeps_done : -1; }
 
+int clv_launch_info(const clv_sampler* s, int64_t* out) {
+  if (!s || !out) return fail(CLV_EINVAL, "null argument");
+  out[0] = s->persistent ? 1 : 0;
+  out[1] = s->persist_bpc;
+  out[2] = s->n_cu;
+  out[3] = (int64_t)(s->g.nb_local + (s->persistent ? 1 : 0)) * s->g.n_chains;
+  return CLV_OK;
+}
+
 int clv_set_stream(clv_sampler* s, uint64_t stream) {
   if (!s || !stream) return fail(CLV_EINVAL, "bad arguments");
   if (s->graph_exec) {
@@ -505,6 +529,41 @@ int clv_note_sweeps(clv_sampler* s, int64_t n) {
   return CLV_OK;
 }
 
+namespace {
+// Persistent path: one launch of persist_kernel for all n sweeps (see kernels.hip).
+int run_persistent(clv_sampler* s, int64_t n_sweeps) {
+  if (n_sweeps == 0) return CLV_OK;
+  // every hand-off slot empty (all-ones bytes: the sentinel NaN)
+  CLV_HIP(hipMemsetAsync(s->d_hyp2, 0xFF, sizeof(double) * 2 * s->g.n_chains * HS, s->stream));
+  CLV_HIP(hipMemsetAsync(s->d_block, 0xFF, sizeof(double) * s->g.n_chains * s->g.blocks_per_rank * s->g.stride, s->stream));
+  SweepArgs a = sweep_args(s, 0, 1);
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (s->timing) {
+    int rc = ensure_events(s);
+    if (rc) return rc;
+    e0 = s->ev[4 * s->ev_used];
+    e1 = s->ev[4 * s->ev_used + 1];
+    if (s->ev_sweeps.size() < TIMING_EVENTS) s->ev_sweeps.assign(TIMING_EVENTS, 1);
+    s->ev_sweeps[s->ev_used] = n_sweeps;
+  }
+  CLV_HIP(launch_persist(a, s->sweeps_done + 1, n_sweeps, s->stream, e0, e1));
+  if (s->timing) {
+    s->ev_used++;
+    int rc = harvest_timing(s);
+    if (rc) return rc;
+  }
+  CLV_HIP(hipStreamSynchronize(s->stream));
+  uint32_t ab = 0;
+  CLV_HIP(hipMemcpy(&ab, &s->d_ctrl->abort, sizeof(uint32_t), hipMemcpyDeviceToHost));
+  if (ab) {
+    (void)hipMemset(&s->d_ctrl->abort, 0, sizeof(uint32_t));
+    return fail(CLV_EHIP, "persistent sweep kernel: a workgroup waited > 2 s for its chain (not all resident?)");
+  }
+  s->sweeps_done += n_sweeps;
+  return CLV_OK;
+}
+}  // namespace
+
 int clv_run(clv_sampler* s, int64_t n_sweeps) {
   if (!s) return fail(CLV_EINVAL, "null sampler");
   if (s->g.world_size != 1) return fail(CLV_ESTATE, "clv_run is unsharded; use clv_sweep/clv_hyper");
@@ -517,6 +576,7 @@ int clv_run(clv_sampler* s, int64_t n_sweeps) {
     if (rc) return rc;
     s->pending_init_hyper = false;
   }
+  if (s->persistent) return run_persistent(s, n_sweeps);
   int64_t left = n_sweeps;
   if (s->timing) {
     rc = ensure_events(s);
@@ -664,7 +724,7 @@ int clv_debug_wg_stamps(clv_sampler* s, uint64_t* out) {
   if (!s || !out) return fail(CLV_EINVAL, "null argument");
   if (!s->d_stamps) return fail(CLV_ESTATE, "library not built with CLV_STAMPS (make STAMPS=1)");
   CLV_HIP(hipStreamSynchronize(s->stream));
-  CLV_HIP(hipMemcpy(out, s->d_stamps + 1024 * 8, sizeof(uint64_t) * 12 * s->g.n_chains * s->g.nb_local,
+  CLV_HIP(hipMemcpy(out, s->d_stamps + 1024 * 8, sizeof(uint64_t) * 12 * s->g.n_chains * (s->g.nb_local + 1),
                     hipMemcpyDeviceToHost));
   return CLV_OK;
 }

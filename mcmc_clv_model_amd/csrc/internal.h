@@ -73,6 +73,9 @@ struct clv_sampler {
   double* d_prior = nullptr;
   clv::Ctrl* d_ctrl = nullptr;
   uint32_t* d_arrive = nullptr;     // fused-tail arrival counters: [chain], then [chain][units_per_rank]
+  double* d_hyp2 = nullptr;         // persistent kernel: [2][chain][HS] hand-off slots
+  bool persistent = false;          // clv_run uses persist_kernel (all workgroups resident)
+  int persist_bpc = 0, n_cu = 0;    // persist_kernel occupancy (workgroups per CU), CUs
   double* d_hvar = nullptr;         // [chain][HV] precomputed hyper variates
   unsigned long long* d_stamps = nullptr;  // CLV_STAMPS diagnostic build only
   double *d_level1 = nullptr, *d_level2 = nullptr, *d_loglik = nullptr, *d_sums = nullptr;
@@ -88,6 +91,7 @@ struct clv_sampler {
 
   bool timing = false;
   std::vector<hipEvent_t> ev;  // 4 per slot: sweep start/end, hyper start/end
+  std::vector<int64_t> ev_sweeps;  // sweeps per timed launch (persistent launches time many)
   int ev_used = 0;
   double t_sweep_ms = 0.0, t_hyper_ms = 0.0;
   int64_t n_sweep_timed = 0, n_hyper_timed = 0;

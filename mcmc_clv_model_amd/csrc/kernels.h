@@ -25,7 +25,7 @@ enum : int {
 struct Ctrl {
   int64_t cur;        // sweeps completed; the next sweep kernel runs sweep cur + 1
   uint32_t arrive;    // arrival counter of the hyper kernel's workgroups
-  uint32_t pad;
+  uint32_t abort;     // persistent kernel: a wait timed out (host checks and clears it)
 };
 
 struct Geometry {
@@ -85,6 +85,8 @@ struct SweepArgs {
   const double* hyper;       // [chain][HS]
   double* blockpart;         // [chain][stride][blocks_per_rank]
   const Ctrl* ctrl;
+  Ctrl* ctrl_rw;             // persistent kernel: writes cur and abort
+  double* hyp2;              // persistent kernel: [2][chain][HS] (beta, Sigma) hand-off slots by sweep parity
   double* level1;            // [chain][n_draws][n][D+2] or null
   double* sums;              // [chain][CLV_N_SUM_STATS][n] or null
   int64_t* n_stored;         // device counter of stored draws (chain 0 block 0 bumps it)
@@ -111,6 +113,9 @@ struct GroupArgs {
 hipError_t launch_sweep(const SweepArgs& a, bool replay, hipStream_t st, hipEvent_t e0 = nullptr,
                         hipEvent_t e1 = nullptr);
 hipError_t launch_group(const GroupArgs& a, hipStream_t st);
+hipError_t launch_persist(const SweepArgs& a, int64_t s_first, int64_t n_sweeps, hipStream_t st,
+                          hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
+hipError_t persist_occupancy(int D, int K, int* blocks_per_cu);
 hipError_t launch_hyper(const HyperArgs& a, bool replay, hipStream_t st);
 hipError_t launch_set_hyper(int D, int K, int n_chains, double* hyper, const double* beta_sigma,
                             double omega2, hipStream_t st);

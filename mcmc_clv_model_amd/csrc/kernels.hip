@@ -170,7 +170,13 @@ __device__ __forceinline__ void wg_stamp(unsigned long long* st, int64_t wg, int
   st[1024 * 8 + wg * 12 + k] = v;
 }
 #define CLV_WG_STAMP(st, wg, k) wg_stamp(st, wg, k)
+// persistent kernel: the same per-workgroup record, s_memrealtime only, for one chosen sweep
+#define CLV_P_STAMP(st, wg, k, on) \
+  do {                             \
+    if ((on) && (st)) (st)[1024 * 8 + (wg) * 12 + (k)] = (k) == 8 ? __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)) : (k) == 9 ? __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11)) : __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
 #else
+#define CLV_P_STAMP(st, wg, k, on) ((void)0)
 #define CLV_WG_STAMP(st, wg, k) ((void)0)
 #define CLV_STAMP(st, s, k, is_min) ((void)0)
 #endif
@@ -228,38 +234,52 @@ __device__ void cholesky(const double (&A)[D][D], double (&L)[D][D]) {
   }
 }
 
+// Hyper-state writes are write-through (sc1): a persistent sweep kernel reads them on other CUs in
+// the same launch, after the chain's release flag.
+__device__ __forceinline__ void hstore(double* H, int idx, double v) {
+  __hip_atomic_store(H + idx, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// TO_LDS: plain stores into a workgroup-local block (the persistent kernel's tail publishes it
+// with one coalesced store per lane)
+template <bool TO_LDS>
+__device__ __forceinline__ void hput(double* H, int idx, double v) {
+  if constexpr (TO_LDS) H[idx] = v;
+  else hstore(H, idx, v);
+}
+
 // hyper-state finalisation from (beta, Sigma): inverse block, proposal scales, eta constants.
-template <int D, int K>
+template <int D, int K, bool TO_LDS = false>
 __device__ void finalize_hyper(const double* beta_flat, const double (&Sig)[D][D], double omega2, double* H) {
 #pragma unroll
-  for (int q = 0; q < K * D; ++q) H[H_BETA + q] = beta_flat[q];
-  for (int q = 0; q < 9; ++q) H[H_SIGMA + q] = 0.0;
+  for (int q = 0; q < K * D; ++q) hput<TO_LDS>(H, H_BETA + q, beta_flat[q]);
+  for (int q = 0; q < 9; ++q) hput<TO_LDS>(H, H_SIGMA + q, 0.0);
 #pragma unroll
   for (int p = 0; p < D; ++p)
 #pragma unroll
-    for (int q = 0; q < D; ++q) H[H_SIGMA + p * 3 + q] = Sig[p][q];
+    for (int q = 0; q < D; ++q) hput<TO_LDS>(H, H_SIGMA + p * 3 + q, Sig[p][q]);
   if constexpr (D == 2) {
     const double det = Sig[0][0] * Sig[1][1] - Sig[0][1] * Sig[1][0];
-    H[H_P00] = Sig[1][1] / det;
-    H[H_P01] = -Sig[0][1] / det;
-    H[H_P11] = Sig[0][0] / det;
+    hput<TO_LDS>(H, H_P00, Sig[1][1] / det);
+    hput<TO_LDS>(H, H_P01, -Sig[0][1] / det);
+    hput<TO_LDS>(H, H_P11, Sig[0][0] / det);
   } else {
     // top-left 2x2 block of the full 3x3 inverse (tri:402 with tri:422-424; quirk Q4)
     const double c00 = Sig[1][1] * Sig[2][2] - Sig[1][2] * Sig[2][1];
     const double c01 = Sig[1][0] * Sig[2][2] - Sig[1][2] * Sig[2][0];
     const double c02 = Sig[1][0] * Sig[2][1] - Sig[1][1] * Sig[2][0];
     const double det = Sig[0][0] * c00 - Sig[0][1] * c01 + Sig[0][2] * c02;
-    H[H_P00] = c00 / det;
-    H[H_P01] = -(Sig[0][1] * Sig[2][2] - Sig[0][2] * Sig[2][1]) / det;
-    H[H_P11] = (Sig[0][0] * Sig[2][2] - Sig[0][2] * Sig[2][0]) / det;
-    H[H_S22] = Sig[2][2];
+    hput<TO_LDS>(H, H_P00, c00 / det);
+    hput<TO_LDS>(H, H_P01, -(Sig[0][1] * Sig[2][2] - Sig[0][2] * Sig[2][1]) / det);
+    hput<TO_LDS>(H, H_P11, (Sig[0][0] * Sig[2][2] - Sig[0][2] * Sig[2][0]) / det);
+    hput<TO_LDS>(H, H_S22, Sig[2][2]);
     const double post_var = 1.0 / (1.0 / omega2 + 1.0 / Sig[2][2]);  // tri:325-326
-    H[H_POSTVAR] = post_var;
-    H[H_SQRT_POSTVAR] = sqrt(post_var);
-    H[H_OMEGA2] = omega2;
+    hput<TO_LDS>(H, H_POSTVAR, post_var);
+    hput<TO_LDS>(H, H_SQRT_POSTVAR, sqrt(post_var));
+    hput<TO_LDS>(H, H_OMEGA2, omega2);
   }
-  H[H_S00] = Sig[0][0];
-  H[H_S11] = Sig[1][1];
+  hput<TO_LDS>(H, H_S00, Sig[0][0]);
+  hput<TO_LDS>(H, H_S11, Sig[1][1]);
 }
 
 // LDS scratch of the level-2 draw.
@@ -271,6 +291,7 @@ struct L2Scratch {
   double Sig[9];             // Sigma                  [p*D + q]
   double Ls[9];              // chol(Sigma)            [p*D + q]
   double beta[CLV_MAX_K * 3];// beta = B_hat + w       [k*D + d] (= beta.ravel() row-major)
+  double Ai[9];              // Philox mode: inverse Bartlett factor (persistent kernel: formed early)
 };
 
 // Orders LDS accesses between the lanes of one wavefront (LDS operations of a wave complete in
@@ -294,7 +315,7 @@ __device__ __forceinline__ void stage_prior(const double* prior, L2Scratch* sc) 
 // iwn: n_tril normals, chi2: D chi-square draws, noise: either the replayed mvn noise (w, D*K)
 // or standard normals z (D*K) mapped through kron(chol(Sigma), chol(V)).
 template <int D, int K>
-__device__ void level2_draw(const double* tot, const double* iwn, const double* chi2, const double* noise,
+__device__ void level2_draw_exact(const double* tot, const double* iwn, const double* chi2, const double* noise,
                             bool noise_is_w, L2Scratch* sc) {
   constexpr int NXY = K * D;
   const int t = threadIdx.x;
@@ -403,6 +424,213 @@ __device__ void level2_draw(const double* tot, const double* iwn, const double* 
   wave_sync();
 }
 
+// Inverse of the Bartlett factor A (lower triangular: A[p][p] = sqrt(chi2[p]), strict lower part
+// the iw normals in np.tril_indices(D, -1) order).  Depends on the variates only, so the
+// persistent kernel's level-2 workgroup forms it while the sweep runs.
+template <int D>
+__device__ __forceinline__ void bartlett_inverse(const double* iwn, const double* chi2, double* Ai /* [D*D] */) {
+  double A[D][D], I[D][D];
+  {
+    int m = 0;
+#pragma unroll
+    for (int p = 0; p < D; ++p)
+#pragma unroll
+      for (int q = 0; q < D; ++q) A[p][q] = 0.0;
+#pragma unroll
+    for (int p = 1; p < D; ++p)
+#pragma unroll
+      for (int q = 0; q < p; ++q) A[p][q] = iwn[m++];
+#pragma unroll
+    for (int p = 0; p < D; ++p) A[p][p] = sqrt(chi2[p]);
+  }
+#pragma unroll
+  for (int j = 0; j < D; ++j) {
+#pragma unroll
+    for (int q = 0; q < D; ++q) I[j][q] = 0.0;
+    I[j][j] = 1.0 / A[j][j];
+  }
+#pragma unroll
+  for (int i = 1; i < D; ++i)
+#pragma unroll
+    for (int j = 0; j < i; ++j) {
+      double sv = 0.0;
+#pragma unroll
+      for (int k = j; k < i; ++k) sv += A[i][k] * I[k][j];
+      I[i][j] = -(sv * I[i][i]);
+    }
+#pragma unroll
+  for (int p = 0; p < D; ++p)
+#pragma unroll
+    for (int q = 0; q < D; ++q) Ai[p * D + q] = I[p][q];
+}
+
+// Philox-mode core (one lane): Sigma = (L A^-1)(L A^-1)' with L = chol(S_n) — the Bartlett form of
+// level2_draw_exact with A^-1 applied by multiplication instead of a triangular solve.  M = L A^-1
+// is lower triangular with a positive diagonal, so it IS chol(Sigma): no second factorisation.
+template <int D>
+__device__ __forceinline__ void iw_core_fast(const double (&Sn)[D][D], const double* Ai, double (&Sig)[D][D],
+                                             double (&M)[D][D]) {
+  double L[D][D];
+  cholesky<D>(Sn, L);
+#pragma unroll
+  for (int r = 0; r < D; ++r)
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      double sv = 0.0;
+#pragma unroll
+      for (int k = j; k <= r; ++k) sv += L[r][k] * Ai[k * D + j];
+      M[r][j] = j <= r ? sv : 0.0;
+    }
+#pragma unroll
+  for (int p = 0; p < D; ++p)
+#pragma unroll
+    for (int q = 0; q <= p; ++q) {
+      double sv = 0.0;
+#pragma unroll
+      for (int k = 0; k <= q; ++k) sv += M[p][k] * M[q][k];
+      Sig[p][q] = sv;
+      Sig[q][p] = sv;
+    }
+}
+
+// Philox-mode level-2 draw.  Small K*D (the persistent kernel's sizes): lane 0 alone, all in
+// registers — no LDS round trips between phases, which dominate at these sizes; larger K: the
+// element-parallel phases of level2_draw_exact around the fast core.  `Ai`: the Bartlett inverse
+// if already formed (LDS), else null.  Every path (fused, sharded, persistent) calls this same
+// function in Philox mode, so they stay bitwise identical.
+template <int D, int K>
+__device__ void level2_draw_fast(const double* tot, const double* iwn, const double* chi2, const double* noise,
+                                 const double* Ai_pre, L2Scratch* sc) {
+  constexpr int NXY = K * D;
+  const int t = threadIdx.x;
+  if (t >= 64) return;
+  const double* V = sc->prior;
+  const double* cholV = sc->prior + 81;
+  const double* A0B0 = sc->prior + 162;
+  const double* S0B = sc->prior + 189;
+  if constexpr (NXY <= 12) {
+    if (t == 0) {
+      double Ai[D * D];
+      if (Ai_pre) {
+#pragma unroll
+        for (int q = 0; q < D * D; ++q) Ai[q] = Ai_pre[q];
+      } else {
+        bartlett_inverse<D>(iwn, chi2, Ai);
+      }
+      double R[NXY], Bh[NXY];
+#pragma unroll
+      for (int q = 0; q < NXY; ++q) R[q] = tot[q] + A0B0[q];
+#pragma unroll
+      for (int q = 0; q < NXY; ++q) {  // B_hat[k][d] = sum_j V[k][j] R[j][d]
+        const int k = q / D, d = q % D;
+        double sv = 0.0;
+#pragma unroll
+        for (int j = 0; j < K; ++j) sv += V[k * K + j] * R[j * D + d];
+        Bh[q] = sv;
+      }
+      double Sn[D][D];
+      int n = NXY;
+#pragma unroll
+      for (int p = 0; p < D; ++p)
+#pragma unroll
+        for (int q = p; q < D; ++q) {
+          double rb = 0.0;
+#pragma unroll
+          for (int k = 0; k < K; ++k) rb += R[k * D + p] * Bh[k * D + q];
+          Sn[p][q] = (S0B[p * D + q] + tot[n++]) - rb;
+          Sn[q][p] = Sn[p][q];
+        }
+      double Sig[D][D], M[D][D];
+      iw_core_fast<D>(Sn, Ai, Sig, M);
+#pragma unroll
+      for (int q = 0; q < NXY; ++q) {  // beta = B_hat + kron(chol Sigma, chol V) z, row-major ravel (Q1)
+        const int p = q / K, bq = q % K;
+        double sv = 0.0;
+#pragma unroll
+        for (int cc = 0; cc <= p; ++cc)
+#pragma unroll
+          for (int e = 0; e <= bq; ++e) sv += M[p][cc] * cholV[bq * K + e] * noise[cc * K + e];
+        sc->beta[q] = Bh[q] + sv;
+      }
+#pragma unroll
+      for (int p = 0; p < D; ++p)
+#pragma unroll
+        for (int q = 0; q < D; ++q) sc->Sig[p * D + q] = Sig[p][q];
+    }
+    wave_sync();
+  } else {
+    if (t < NXY) sc->R[t] = tot[t] + A0B0[t];
+    wave_sync();
+    if (t < NXY) {
+      const int k = t / D, d = t % D;
+      double sv = 0.0;
+#pragma unroll
+      for (int j = 0; j < K; ++j) sv += V[k * K + j] * sc->R[j * D + d];
+      sc->Bh[t] = sv;
+    }
+    wave_sync();
+    if (t < D * (D + 1) / 2) {
+      int p = 0, q = t;
+      while (q >= D - p) {
+        q -= D - p;
+        ++p;
+      }
+      q += p;
+      double rb = 0.0;
+#pragma unroll
+      for (int k = 0; k < K; ++k) rb += sc->R[k * D + p] * sc->Bh[k * D + q];
+      sc->Sn[t] = (S0B[p * D + q] + tot[NXY + t]) - rb;
+    }
+    wave_sync();
+    if (t == 0) {
+      double Ai[D * D];
+      if (Ai_pre) {
+#pragma unroll
+        for (int q = 0; q < D * D; ++q) Ai[q] = Ai_pre[q];
+      } else {
+        bartlett_inverse<D>(iwn, chi2, Ai);
+      }
+      double Sn[D][D];
+      int n = 0;
+#pragma unroll
+      for (int p = 0; p < D; ++p)
+#pragma unroll
+        for (int q = p; q < D; ++q) {
+          Sn[p][q] = sc->Sn[n];
+          Sn[q][p] = sc->Sn[n++];
+        }
+      double Sig[D][D], M[D][D];
+      iw_core_fast<D>(Sn, Ai, Sig, M);
+#pragma unroll
+      for (int p = 0; p < D; ++p)
+#pragma unroll
+        for (int q = 0; q < D; ++q) {
+          sc->Sig[p * D + q] = Sig[p][q];
+          sc->Ls[p * D + q] = M[p][q];
+        }
+    }
+    wave_sync();
+    if (t < NXY) {
+      const int p = t / K, bq = t % K;
+      double sv = 0.0;
+      for (int cc = 0; cc <= p; ++cc)
+        for (int e = 0; e <= bq; ++e) sv += sc->Ls[p * D + cc] * cholV[bq * K + e] * noise[cc * K + e];
+      sc->beta[t] = sc->Bh[t] + sv;
+    }
+    wave_sync();
+  }
+}
+
+// Level-2 draw: replay mode follows the reference's operation order (level2_draw_exact, bitwise
+// trajectories); Philox mode takes the latency-optimised form.
+template <int D, int K>
+__device__ __forceinline__ void level2_draw(const double* tot, const double* iwn, const double* chi2,
+                                            const double* noise, bool noise_is_w, L2Scratch* sc,
+                                            const double* Ai_pre = nullptr) {
+  if (noise_is_w) level2_draw_exact<D, K>(tot, iwn, chi2, noise, true, sc);
+  else level2_draw_fast<D, K>(tot, iwn, chi2, noise, Ai_pre, sc);
+}
+
 // Philox-mode hyper variates (fp64).
 __device__ double hyper_normal(uint32_t k0, uint32_t k1, uint32_t slot, uint32_t sweep) {
   const u32x4 r = hyper_block(k0, k1, slot, sweep);
@@ -504,9 +732,9 @@ __device__ void hyper_body(const HyperArgs& a, int c, int64_t s, int mode, const
 #pragma unroll
         for (int r = p; r < D; ++r) o[q++] = Sig[p][r];  // bi:412, tri:550-554
     }
-    if (mode == 0 && is_stored(s, g))
+    if (mode != 1 && is_stored(s, g))
       a.loglik[(int64_t)c * g.n_draws + draw_index(s, g)] = tot[NS - 1] / (double)g.n_global;  // np.mean
-    if (mode == 0) {
+    if (mode == 0) {  // (mode 2, the persistent kernel, keeps the sweep index itself)
       // the last chain to finish advances the sweep counter (every workgroup of this launch has
       // read it before arriving)
       // relaxed: the next launch reads cur and the hyper state after the kernel boundary (whose
@@ -569,10 +797,12 @@ __device__ __forceinline__ void cust_load(Cust<D, K>& u, const SweepArgs& a, int
   u.gi = (uint32_t)(g.shard_begin + i);
 }
 
-// Phase A2 (bi:193-227, bi:280-290): draw_z, draw_tau, log-posterior constants.
+// Phase A2a (bi:193-227): draw_z, draw_tau and the log-scale state — independent of the level-2
+// state (beta, Sigma), so the persistent kernel runs it for sweep s+1 while sweep s's level-2
+// draw is still in flight.
 template <int D, int K, bool REPLAY>
-__device__ __forceinline__ void cust_prepare(Cust<D, K>& u, const SweepArgs& a, int c, int64_t s, const double* H,
-                                             uint32_t k0, uint32_t k1, const double* tape, const double* exp_tab) {
+__device__ __forceinline__ void cust_ztau(Cust<D, K>& u, const SweepArgs& a, int64_t s, uint32_t k0, uint32_t k1,
+                                          const double* tape, const double* exp_tab) {
   const Geometry& g = a.g;
   const int64_t i = u.i;
   const double lam = u.lam, mu = u.mu;
@@ -622,7 +852,17 @@ __device__ __forceinline__ void cust_prepare(Cust<D, K>& u, const SweepArgs& a, 
     tau = -log((1 - uu) * e_tx + uu * e_T) / ml;
   }
   u.tau = tau;
+  u.lc.xm = u.xm;
+  u.lc.omz = z ? 0.0 : 1.0;
+  u.lc.w = z ? T : tau;
+  u.ll = log(lam);
+  u.lm = log(mu);
+}
 
+// Phase A2b (bi:280-290): log-posterior constants from (beta, Sigma) and the current point's
+// log posterior.
+template <int D, int K, bool REPLAY>
+__device__ __forceinline__ void cust_coeffs(Cust<D, K>& u, const double* H, const double* exp_tab) {
   // ---- _draw_level_1 (bi:268-339): mv_mean = X @ beta (bi:284)
   double m0 = 0.0, m1 = 0.0;
 #pragma unroll
@@ -631,16 +871,11 @@ __device__ __forceinline__ void cust_prepare(Cust<D, K>& u, const SweepArgs& a, 
     m1 += u.xr[k] * H[H_BETA + k * D + 1];
   }
   LPConst& lc = u.lc;
-  lc.xm = u.xm;
-  lc.omz = z ? 0.0 : 1.0;
-  lc.w = z ? T : tau;
   lc.m0 = m0;
   lc.m1 = m1;
   lc.p00 = H[H_P00];
   lc.p01 = H[H_P01];
   lc.p11 = H[H_P11];
-  u.ll = log(lam);
-  u.lm = log(mu);
   if constexpr (REPLAY) {
     u.cur = log_post(lc, u.ll, u.lm);
   } else {
@@ -655,6 +890,15 @@ __device__ __forceinline__ void cust_prepare(Cust<D, K>& u, const SweepArgs& a, 
   }
 }
 
+// Phase A2 (bi:193-227, bi:280-290): both of the above.
+template <int D, int K, bool REPLAY>
+__device__ __forceinline__ void cust_prepare(Cust<D, K>& u, const SweepArgs& a, int c, int64_t s, const double* H,
+                                             uint32_t k0, uint32_t k1, const double* tape, const double* exp_tab) {
+  (void)c;
+  cust_ztau<D, K, REPLAY>(u, a, s, k0, k1, tape, exp_tab);
+  cust_coeffs<D, K, REPLAY>(u, H, exp_tab);
+}
+
 // One Philox-mode MH step (bi:316-335) with lp(proposal) = -inf for pm > 5 (Q3): accept iff
 // pm <= 5 and exp(plp - cur) > u  <=>  plp - cur > log(u)  (cur = -inf accepts any finite one).
 template <int D, int K>
@@ -663,19 +907,54 @@ __device__ __forceinline__ void mh_step(Cust<D, K>& u, double s00, double s11, f
   const double pl = clip70(__builtin_fma(s00, (double)t_l, u.ll));
   const double pm = clip70(__builtin_fma(s11, (double)t_m, u.lm));
   const double plp = log_post_fast(u.fc, pl, pm, exp_tab);
-  if (pm <= 5.0 && (plp - u.cur) > (double)l_u) {
-    u.ll = pl;
-    u.lm = pm;
-    u.cur = plp;
-  }
+  // selects, not a branch: keeps a chunk's steps in one basic block with the next chunk's variates
+  const bool acc = (pm <= 5.0) & ((plp - u.cur) > (double)l_u);
+  u.ll = acc ? pl : u.ll;
+  u.lm = acc ? pm : u.lm;
+  u.cur = acc ? plp : u.cur;
 }
 
-// Phase C: state update (bi:337-338), draw_eta (tri:306-333), storage (bi:402-428, tri:539-571),
-// the customer's sufficient statistics into acc.
+// The sweep's S Philox-mode MH steps.  Software pipeline: the Philox blocks and t3 transforms of
+// the next chunk of MH_CHUNK_STEPS steps are independent of the state; each full chunk's steps and
+// the next chunk's variates form one branch-free basic block, so the scheduler can interleave
+// that work with the dependent fp64 accept/reject chain.  The last chunk's steps beyond S are
+// padded with log U = +inf (never accepted: the state is unchanged) instead of a branch.
+template <int D, int K>
+__device__ __forceinline__ void mh_run(Cust<D, K>& cu, const SlotPhilox& ph, double s00, double s11, int S,
+                                       const double* exp_tab) {
+  constexpr int MC = MH_CHUNK_STEPS;
+  const int n_chunks = (S + MC - 1) / MC;
+  if (n_chunks <= 0) return;
+  float tl[MC], tm[MC], lu[MC];
+  mh_chunk_variates(ph, 0u, tl, tm, lu);
+  for (int ch = 0; ch + 1 < n_chunks; ++ch) {
+    float ntl[MC], ntm[MC], nlu[MC];
+    mh_chunk_variates(ph, (uint32_t)(ch + 1), ntl, ntm, nlu);
+#pragma unroll
+    for (int st = 0; st < MC; ++st) mh_step(cu, s00, s11, tl[st], tm[st], lu[st], exp_tab);
+#pragma unroll
+    for (int st = 0; st < MC; ++st) {
+      tl[st] = ntl[st];
+      tm[st] = ntm[st];
+      lu[st] = nlu[st];
+    }
+  }
+  const int rem = S - (n_chunks - 1) * MC;
+#pragma unroll
+  for (int st = 0; st < MC; ++st) mh_step(cu, s00, s11, tl[st], tm[st], st < rem ? lu[st] : __builtin_inff(), exp_tab);
+}
+
+// Phase C1: state update (bi:337-338), draw_eta (tri:306-333), the likelihood term of stored
+// sweeps (bi:423-427) and the customer's sufficient statistics into acc.
+template <int D>
+struct CustOut {
+  double lam, mu, eta, lgl, lgm;
+};
+
 template <int D, int K, bool REPLAY, int NS>
-__device__ __forceinline__ void cust_finish(Cust<D, K>& u, const SweepArgs& a, int c, int64_t s, bool stored,
-                                            const double* H, uint32_t k0, uint32_t k1, const double* tape,
-                                            const double* exp_tab, double (&acc)[NS]) {
+__device__ __forceinline__ CustOut<D> cust_finish(Cust<D, K>& u, const SweepArgs& a, int64_t s, bool stored,
+                                                  const double* H, uint32_t k0, uint32_t k1, const double* tape,
+                                                  const double* exp_tab, double (&acc)[NS]) {
   constexpr int NXY = K * D;
   const Geometry& g = a.g;
   const int64_t i = u.i;
@@ -684,7 +963,6 @@ __device__ __forceinline__ void cust_finish(Cust<D, K>& u, const SweepArgs& a, i
   double lam = REPLAY ? exp(u.ll) : exp_fast(u.ll, exp_tab);
   double mu = REPLAY ? exp(u.lm) : exp_fast(u.lm, exp_tab);
   double eta = 1.0, Y[D];
-  const bool z = u.z;
   if constexpr (D == 3) {
     double m2 = 0.0;
 #pragma unroll
@@ -704,46 +982,23 @@ __device__ __forceinline__ void cust_finish(Cust<D, K>& u, const SweepArgs& a, i
     Y[1] = REPLAY ? log(mu) : u.lm;
     Y[2] = log(eta);
   }
-  double lik = 0.0;
+  double lik = 0.0, lgl = 0.0, lgm = 0.0;
   if (stored) {
     if constexpr (REPLAY) {
       lam = exp(log(lam));  // quirk Q5 (bi:405-406)
       mu = exp(log(mu));
     }
-    const int64_t dr = draw_index(s, g);
-    if (a.level1) {
-      double* o = a.level1 + (((int64_t)c * g.n_draws + dr) * g.n + i) * (D + 2);
-      o[0] = lam;
-      o[1] = mu;
-      o[2] = u.tau;
-      o[3] = z ? 1.0 : 0.0;
-      if constexpr (D == 3) o[4] = eta;
-    }
-    const double lgl = REPLAY ? log(lam) : u.ll, lgm = REPLAY ? log(mu) : u.lm;
+    lgl = REPLAY ? log(lam) : u.ll;
+    lgm = REPLAY ? log(mu) : u.lm;
     lik = (u.xm * lgl + u.lc.omz * lgm) - (lam + mu) * u.lc.w;  // bi:423-427
-    if (a.sums) {
-      double* sm = a.sums + (int64_t)c * CLV_N_SUM_STATS * g.n + i;
-      sm[CLV_SUM_LAMBDA * g.n] += lam;
-      sm[CLV_SUM_MU * g.n] += mu;
-      sm[CLV_SUM_Z * g.n] += z ? 1.0 : 0.0;
-      sm[CLV_SUM_LOG_LAMBDA * g.n] += lgl;
-      sm[CLV_SUM_LOG_MU * g.n] += lgm;
-      sm[CLV_SUM_LAMBDA2 * g.n] += lam * lam;
-      sm[CLV_SUM_MU2 * g.n] += mu * mu;
-      if constexpr (D == 3) {
-        sm[CLV_SUM_ETA * g.n] += eta;
-        sm[CLV_SUM_LOG_ETA * g.n] += log(eta);
-      }
-    }
   }
   if constexpr (D == 2) {
     // bi: the next level-2 draw uses log of the carried state (bi:393)
     Y[0] = REPLAY ? log(lam) : u.ll;
     Y[1] = REPLAY ? log(mu) : u.lm;
   }
-  const int64_t ci = (int64_t)c * g.n + i;
-  a.lam[ci] = lam;
-  a.mu[ci] = mu;
+  u.lam = lam;
+  u.mu = mu;
   // ---- sufficient statistics: X'Y (K x D), Y'Y (upper triangle), likelihood term
 #pragma unroll
   for (int k = 0; k < K; ++k)
@@ -755,11 +1010,48 @@ __device__ __forceinline__ void cust_finish(Cust<D, K>& u, const SweepArgs& a, i
 #pragma unroll
     for (int q = p; q < D; ++q) acc[t++] += Y[p] * Y[q];
   acc[NS - 1] += lik;
+  return CustOut<D>{lam, mu, eta, lgl, lgm};
 }
 
-// One workgroup = one statistics block of BLOCK customers of one chain, one customer per lane.
-// (Two interleaved customers per lane for ILP at CDNOW size measured slower — 35 vs 23 us/sweep —
-// and would tie the statistics' summation order to the lane mapping.)
+// Phase C2: storage (bi:402-412, tri:539-571) — issued after the workgroup's partial has been
+// handed off, so the hand-off's store drain does not wait for them — and the carried state.
+template <int D, int K>
+__device__ __forceinline__ void cust_store(const Cust<D, K>& u, const CustOut<D>& o, const SweepArgs& a, int c,
+                                           int64_t s, bool stored, bool store_state) {
+  const Geometry& g = a.g;
+  const int64_t i = u.i;
+  if (stored) {
+    const int64_t dr = draw_index(s, g);
+    if (a.level1) {
+      double* w = a.level1 + (((int64_t)c * g.n_draws + dr) * g.n + i) * (D + 2);
+      w[0] = o.lam;
+      w[1] = o.mu;
+      w[2] = u.tau;
+      w[3] = u.z ? 1.0 : 0.0;
+      if constexpr (D == 3) w[4] = o.eta;
+    }
+    if (a.sums) {
+      double* sm = a.sums + (int64_t)c * CLV_N_SUM_STATS * g.n + i;
+      sm[CLV_SUM_LAMBDA * g.n] += o.lam;
+      sm[CLV_SUM_MU * g.n] += o.mu;
+      sm[CLV_SUM_Z * g.n] += u.z ? 1.0 : 0.0;
+      sm[CLV_SUM_LOG_LAMBDA * g.n] += o.lgl;
+      sm[CLV_SUM_LOG_MU * g.n] += o.lgm;
+      sm[CLV_SUM_LAMBDA2 * g.n] += o.lam * o.lam;
+      sm[CLV_SUM_MU2 * g.n] += o.mu * o.mu;
+      if constexpr (D == 3) {
+        sm[CLV_SUM_ETA * g.n] += o.eta;
+        sm[CLV_SUM_LOG_ETA * g.n] += log(o.eta);
+      }
+    }
+  }
+  if (store_state) {
+    const int64_t ci = (int64_t)c * g.n + i;
+    a.lam[ci] = o.lam;
+    a.mu[ci] = o.mu;
+  }
+}
+
 static_assert(BLOCK == EXP_TAB_N, "the sweep kernel stages the exp table with one entry per lane");
 
 template <int D, int K, bool REPLAY>
@@ -862,6 +1154,7 @@ __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
     }
   }
 
+  CustOut<D> out{};
   if (!a.init && cu.active) {
     const double* H = a.hyper + (int64_t)c * HS;
     uint32_t k0 = 0, k1 = 0;
@@ -896,34 +1189,20 @@ __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
       // Software pipeline: the Philox blocks and t3 transforms of the next chunk of 4 MH steps
       // are independent of the state, so they are generated while the current chunk's fp64
       // accept/reject chain runs (ILP for the ~1.5 waves/SIMD of the CDNOW-sized problem).
-      constexpr int MC = MH_CHUNK_STEPS;
-      float tl[MC], tm[MC], lu[MC];
-      const SlotPhilox ph(k0, k1, cu.gi, (uint32_t)s);
-      const int n_chunks = (g.S + MC - 1) / MC;
       if (threadIdx.x == 0) CLV_WG_STAMP(a.stamps, (int64_t)c * g.nb_local + b, 5);
-      if (n_chunks > 0) mh_chunk_variates(ph, 0u, tl, tm, lu);
-      for (int ch = 0; ch < n_chunks; ++ch) {
-        float ntl[MC], ntm[MC], nlu[MC];
-        if (ch + 1 < n_chunks) mh_chunk_variates(ph, (uint32_t)(ch + 1), ntl, ntm, nlu);
-#pragma unroll
-        for (int st = 0; st < MC; ++st)
-          if (ch * MC + st < g.S) mh_step(cu, s00, s11, tl[st], tm[st], lu[st], exp_tab);  // last chunk may be partial
-#pragma unroll
-        for (int st = 0; st < MC; ++st) {
-          tl[st] = ntl[st];
-          tm[st] = ntm[st];
-          lu[st] = nlu[st];
-        }
-      }
+      mh_run(cu, SlotPhilox(k0, k1, cu.gi, (uint32_t)s), s00, s11, g.S, exp_tab);
     }
     if (threadIdx.x == 0) CLV_WG_STAMP(a.stamps, (int64_t)c * g.nb_local + b, 6);
-    cust_finish<D, K, REPLAY, NS>(cu, a, c, s, stored, H, k0, k1, tape, exp_tab, acc);
+    out = cust_finish<D, K, REPLAY, NS>(cu, a, s, stored, H, k0, k1, tape, exp_tab, acc);
   }
 
   block_reduce<NS>(acc, red, tot);
   if (threadIdx.x < NS)  // sc1 (write-through) store: read cross-CU by the fused tail
     __hip_atomic_store(a.blockpart + ((int64_t)c * g.stride + threadIdx.x) * g.blocks_per_rank + b, tot[threadIdx.x],
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // draws / summaries / state: after the partial (the fused tail's drain below waits only for the
+  // partial's and variates' stores plus these; the tail never reads them)
+  if (!a.init && cu.active) cust_store<D, K>(cu, out, a, c, s, stored, true);
 
   // ---- fused level-2 draw (world_size == 1): no separate hyper launch per sweep.  Two-level
   // hand-off: the last-arriving workgroup of each unit (blocks_per_unit consecutive blocks) sums
@@ -990,6 +1269,260 @@ __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
       hyper_body<D, K, REPLAY, NS, NT>(a.h, c, s, 0, units, red, tot, var_iw, var_chi, var_noise, &l2);
       if (threadIdx.x == 0) CLV_STAMP(a.stamps, s, 3, false);
     }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Persistent sweep kernel (world size 1, Philox mode): one launch runs n_sweeps sweeps.  Grid
+// (nb_local + 1, chains), every workgroup resident at once (checked at create).  Per chain,
+// workgroups 0..nb_local-1 own 256 customers each and keep them in registers for the whole
+// launch; workgroup nb_local is the chain's level-2 workgroup.  Per sweep s:
+//   customers:  wait for (beta, Sigma) of sweep s -> log-posterior constants -> MH -> state,
+//               statistics -> block partial (write-through store) -> draws -> z / tau of s+1
+//   level 2:    variates of the next draw -> wait for all block partials of s -> the fused
+//               path's fixed-order sum -> level-2 draw -> (beta, Sigma) of s+1 published
+// Hand-off without counters or flags: slots are reset to a sentinel (an all-ones NaN, a pattern
+// fp64 arithmetic never produces) and a reader polls (write-through loads) until none of its
+// slots holds the sentinel.  Block partials: one slot set per chain, reset by the level-2
+// workgroup after reading, before it publishes the next (beta, Sigma) — and writers write only
+// after seeing that.  (beta, Sigma): two slot sets by sweep parity; set s&1 is reset (after all
+// readers of s have delivered their partials) before the set of s+1 is written, so a reader of
+// s+2 sees the reset or newer.  Sums are formed in the fused path's order: results are bitwise
+// identical to the launch-per-sweep path.  Every wait is bounded (PERSIST_TIMEOUT): a wave that
+// times out raises ctrl->abort and every wave leaves at its next wait.
+// ---------------------------------------------------------------------------------------------
+constexpr uint64_t PERSIST_TIMEOUT = 200000000ull;  // s_memrealtime ticks (100 MHz): 2 s
+constexpr long long SLOT_EMPTY = -1ll;              // all-ones bit pattern: a NaN no arithmetic yields
+
+__device__ __forceinline__ double ld_wt(const double* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_wt(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool slot_full(double v) { return __double_as_longlong(v) != SLOT_EMPTY; }
+__device__ __forceinline__ double slot_empty() { return __longlong_as_double(SLOT_EMPTY); }
+
+// Bounded wait bookkeeping (uniform): true when this wave must give up.  The abort flag is read
+// every 16th poll only, so a poll iteration costs one memory round trip, not two.
+__device__ __forceinline__ bool wait_expired(uint64_t t0, Ctrl* ctrl, uint32_t poll) {
+  if ((poll & 15u) == 15u && __hip_atomic_load(&ctrl->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return true;
+  if (__builtin_amdgcn_s_memrealtime() - t0 > PERSIST_TIMEOUT) {
+    __hip_atomic_store(&ctrl->abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
+  }
+  return false;
+}
+
+template <int D, int K>
+__global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t s_first, int64_t n_sweeps) {
+  constexpr int NT = BLOCK;
+  constexpr int NXY = K * D;
+  constexpr int NYY = D * (D + 1) / 2;
+  constexpr int NS = NXY + NYY + 1;
+  constexpr int NTRIL = D * (D - 1) / 2;
+  __shared__ double red[BLOCK / 64][NS];
+  __shared__ double tot[NS];
+  __shared__ double exp_tab[EXP_TAB_N];
+  __shared__ double Hs[HS];
+  __shared__ uint32_t s_abort;
+  __shared__ double var_iw[4], var_chi[4], var_noise[32];
+  __shared__ L2Scratch l2;
+  const Geometry& g = a.g;
+  const int c = blockIdx.y;
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int64_t wgi = (int64_t)c * (g.nb_local + 1) + b;
+  const int64_t it_stamp = n_sweeps >= 2 ? n_sweeps - 2 : 0;  // diagnostic build: one sweep's timeline
+  (void)wgi;
+  (void)it_stamp;
+  uint32_t k0, k1;
+  chain_key(a.r.seed, (int64_t)a.r.chain_first + c, &k0, &k1);
+  double* parts = a.blockpart + (int64_t)c * g.stride * g.blocks_per_rank;  // [stat][block]
+  if (tid == 0) s_abort = 0;
+
+  if (b == g.nb_local) {
+    // ================= the chain's level-2 workgroup =================
+    // It shares its CU with customer workgroups; it is on every sweep's critical path, so its
+    // waves take issue priority over theirs (it mostly sleeps in polls otherwise).
+    __builtin_amdgcn_s_setprio(3);
+    stage_prior(a.h.V, &l2);
+    for (int64_t it = 0; it < n_sweeps; ++it) {
+      const int64_t s = s_first + it;
+      const bool stp = tid == 0 && it == it_stamp;
+      (void)stp;
+      const int64_t hs = (D == 2) ? s + 1 : s;  // sweep the drawn (beta, Sigma) belongs to
+      CLV_P_STAMP(a.stamps, wgi, 0, stp);
+      // 1. this draw's variates (as hyper_body without precomputed ones): overlap the sweep
+      if (tid < NTRIL) var_iw[tid] = hyper_normal(k0, k1, HSLOT_NORMAL0 + tid, (uint32_t)hs);
+      if (tid >= 32 && tid < 32 + D * K) var_noise[tid - 32] = hyper_normal(k0, k1, HSLOT_BETA_NORMAL0 + (tid - 32), (uint32_t)hs);
+      if (tid >= 64 && tid < 64 + D) var_chi[tid - 64] = chi2_draw(k0, k1, (uint32_t)hs, tid - 64, a.h.nu_n - D + 1 + (tid - 64));
+      __syncthreads();
+      if (tid == 0) bartlett_inverse<D>(var_iw, var_chi, l2.Ai);  // read back by this lane only
+      CLV_P_STAMP(a.stamps, wgi, 1, stp);
+      // 2. wait for every block partial of sweep s (lane tid: blocks tid, tid + NT, ...; nb <= 2 NT)
+      double v0[NS], v1[NS];
+      const int b0 = tid, b1 = tid + NT;
+      {  // each wavefront polls on its own (no barrier per poll); a lane stops once its slots are full
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        bool done = false;
+        for (uint32_t poll = 0;; ++poll) {
+          if (!done) {
+            bool ok = true;
+#pragma unroll
+            for (int j = 0; j < NS; ++j) {
+              v0[j] = b0 < g.nb_local ? ld_wt(parts + (int64_t)j * g.blocks_per_rank + b0) : 0.0;
+              v1[j] = b1 < g.nb_local ? ld_wt(parts + (int64_t)j * g.blocks_per_rank + b1) : 0.0;
+            }
+#pragma unroll
+            for (int j = 0; j < NS; ++j) ok = ok && slot_full(v0[j]) && slot_full(v1[j]);
+            done = ok;
+          }
+          if (__all(done)) break;
+          if (wait_expired(t0, a.ctrl_rw, poll)) {
+            s_abort = 1;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      __syncthreads();
+      if (s_abort) return;
+      CLV_P_STAMP(a.stamps, wgi, 2, stp);
+      // 3. the fused path's fixed-order sum (hyper_body: lane u sums units u, u + NT, ... in order)
+      double acc[NS];
+#pragma unroll
+      for (int j = 0; j < NS; ++j) {
+        acc[j] = 0.0;
+        if (b0 < g.nb_local) acc[j] += v0[j];
+        if (b1 < g.nb_local) acc[j] += v1[j];
+      }
+      block_reduce<NS, NT>(acc, red, tot);  // also publishes the variates (LDS)
+      CLV_P_STAMP(a.stamps, wgi, 6, stp);
+      // 4. reset: the partial slots (their writers write again only after step 6) and the
+      //    (beta, Sigma) set every reader of s has read (its next write is for s+2)
+#pragma unroll
+      for (int j = 0; j < NS; ++j) {
+        if (b0 < g.nb_local) st_wt(parts + (int64_t)j * g.blocks_per_rank + b0, slot_empty());
+        if (b1 < g.nb_local) st_wt(parts + (int64_t)j * g.blocks_per_rank + b1, slot_empty());
+      }
+      if (it > 0 && tid < HS) st_wt(a.hyp2 + ((int64_t)(s & 1) * g.n_chains + c) * HS + tid, slot_empty());
+      if (tid < HS) Hs[tid] = 0.0;  // unwritten hyper slots publish as 0 (wavefront 0: ordered before the draw's writes)
+      // 5. the draw (wavefront 0) while the resets drain
+      level2_draw<D, K>(tot, var_iw, var_chi, var_noise, false, &l2, l2.Ai);
+      CLV_P_STAMP(a.stamps, wgi, 7, stp);
+      if (tid == 0) {
+        double Sig[D][D];
+#pragma unroll
+        for (int p = 0; p < D; ++p)
+#pragma unroll
+          for (int q = 0; q < D; ++q) Sig[p][q] = l2.Sig[p * D + q];
+        finalize_hyper<D, K, true>(l2.beta, Sig, a.h.omega2, Hs);
+      }
+      CLV_P_STAMP(a.stamps, wgi, 3, stp);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // resets landed (each wave its own)
+      __syncthreads();
+      // 6. publish (beta, Sigma) of sweep s+1: one coalesced write-through store per lane
+      const bool last = it == n_sweeps - 1;
+      if (tid < HS) {
+        if (last) a.h.hyper[(int64_t)c * HS + tid] = Hs[tid];  // the carried state (kernel boundary)
+        else st_wt(a.hyp2 + ((int64_t)((s + 1) & 1) * g.n_chains + c) * HS + tid, Hs[tid]);
+      }
+      CLV_P_STAMP(a.stamps, wgi, 4, stp);
+      CLV_P_STAMP(a.stamps, wgi, 5, tid == 0 && it + 1 == it_stamp);  // the previous sweep's publish
+#ifdef CLV_STAMPS
+      if (tid == 0 && a.stamps && c < 8 && it % 4 == 0 && it / 4 < 1024)  // publish times, every 4th sweep
+        a.stamps[(it / 4) * 8 + c] = __builtin_amdgcn_s_memrealtime();
+#endif
+      // 7. records (off the critical path)
+      const bool store_l2 = hs >= 1 && is_stored(hs, g);
+      double* o = store_l2 ? a.h.level2 + ((int64_t)c * g.n_draws + draw_index(hs, g)) * g.l2w : nullptr;
+      if (tid < K * D && store_l2) o[(tid % D) * K + tid / D] = l2.beta[tid];  // beta.T.ravel() (bi:411)
+      if (tid == 0) {
+        if (store_l2) {
+          int q = K * D;
+#pragma unroll
+          for (int p = 0; p < D; ++p)
+#pragma unroll
+            for (int r = p; r < D; ++r) o[q++] = l2.Sig[p * D + r];  // bi:412, tri:550-554
+        }
+        if (is_stored(s, g)) a.h.loglik[(int64_t)c * g.n_draws + draw_index(s, g)] = tot[NS - 1] / (double)g.n_global;
+        if (last) a.ctrl_rw->cur = s;
+      }
+      __syncthreads();  // LDS (tot, l2, Hs, variates) reused next sweep
+    }
+    return;
+  }
+
+  // ================= customer workgroups =================
+  Cust<D, K> cu;
+  {
+    const int64_t i = (int64_t)b * BLOCK + tid;
+    cu.active = i < g.n;
+    cu.i = cu.active ? i : (g.n > 0 ? g.n - 1 : 0);
+  }
+  cust_load(cu, a, c);  // once per launch: CBS row, covariates, state stay in registers
+  exp_tab[tid] = EXP2_TAB[tid];
+  if (tid < HS) Hs[tid] = a.hyper[(int64_t)c * HS + tid];  // sweep s_first: from before this launch
+  __syncthreads();
+  if (cu.active) cust_ztau<D, K, false>(cu, a, s_first, k0, k1, nullptr, exp_tab);
+  const double* hyp_c = a.hyp2 + (int64_t)c * HS;
+  for (int64_t it = 0; it < n_sweeps; ++it) {
+    const int64_t s = s_first + it;
+    const bool stored = is_stored(s, g);
+    const bool stp = tid == 0 && it == it_stamp;
+    (void)stp;
+    CLV_P_STAMP(a.stamps, wgi, 0, stp);
+    if (it > 0) {  // wait for (beta, Sigma) of sweep s (wavefront 0 polls, one slot per lane)
+      if (tid < 64) {
+        const double* src = hyp_c + (int64_t)(s & 1) * g.n_chains * HS;
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        for (uint32_t poll = 0;; ++poll) {
+          const double v = ld_wt(src + tid);
+          if (__all(slot_full(v))) {
+            Hs[tid] = v;
+            break;
+          }
+          if (wait_expired(t0, a.ctrl_rw, poll)) {
+            if (tid == 0) s_abort = 1;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      __syncthreads();
+      if (s_abort) return;
+    }
+    CLV_P_STAMP(a.stamps, wgi, 1, stp);
+    double acc[NS];
+#pragma unroll
+    for (int j = 0; j < NS; ++j) acc[j] = 0.0;
+    CustOut<D> out{};
+    if (cu.active) {
+      cust_coeffs<D, K, false>(cu, Hs, exp_tab);
+      CLV_P_STAMP(a.stamps, wgi, 2, stp);
+      const double s00 = Hs[H_S00];
+      const double s11 = Hs[H_S11];
+      mh_run(cu, SlotPhilox(k0, k1, cu.gi, (uint32_t)s), s00, s11, g.S, exp_tab);
+      CLV_P_STAMP(a.stamps, wgi, 3, stp);
+      out = cust_finish<D, K, false, NS>(cu, a, s, stored, Hs, k0, k1, nullptr, exp_tab, acc);
+    }
+    CLV_P_STAMP(a.stamps, wgi, 4, stp);
+    block_reduce<NS>(acc, red, tot);
+    if (tid < NS) st_wt(parts + (int64_t)tid * g.blocks_per_rank + b, tot[tid]);
+    CLV_P_STAMP(a.stamps, wgi, 5, stp);
+    CLV_P_STAMP(a.stamps, wgi, 8, stp);
+    CLV_P_STAMP(a.stamps, wgi, 9, stp);
+    if (cu.active) {
+      cust_store<D, K>(cu, out, a, c, s, stored, false);
+      if (it + 1 < n_sweeps) cust_ztau<D, K, false>(cu, a, s + 1, k0, k1, nullptr, exp_tab);
+    }
+    CLV_P_STAMP(a.stamps, wgi, 6, stp);
+  }
+  if (cu.active) {  // the carried state, once per launch
+    const int64_t ci = (int64_t)c * g.n + cu.i;
+    a.lam[ci] = cu.lam;
+    a.mu[ci] = cu.mu;
   }
 }
 
@@ -1103,6 +1636,31 @@ hipError_t launch_sweep(const SweepArgs& a, bool replay, hipStream_t st, hipEven
   CLV_FOR_K(CLV_CASE, 3, false)
   CLV_FOR_K(CLV_CASE, 2, true)
   CLV_FOR_K(CLV_CASE, 3, true)
+#undef CLV_CASE
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_persist(const SweepArgs& a, int64_t s_first, int64_t n_sweeps, hipStream_t st, hipEvent_t e0,
+                          hipEvent_t e1) {
+  const dim3 grid(a.g.nb_local + 1, a.g.n_chains);  // + the chain's level-2 workgroup
+  const dim3 block(BLOCK);
+#define CLV_CASE(DD, KK, RR)                                                                                         \
+  if (a.g.D == DD && a.g.K == KK) {                                                                                \
+    if (e0) hipExtLaunchKernelGGL((persist_kernel<DD, KK>), grid, block, 0, st, e0, e1, 0, a, s_first, n_sweeps); \
+    else hipLaunchKernelGGL((persist_kernel<DD, KK>), grid, block, 0, st, a, s_first, n_sweeps);                  \
+    return hipGetLastError();                                                                                      \
+  }
+  CLV_FOR_K(CLV_CASE, 2, 0)
+  CLV_FOR_K(CLV_CASE, 3, 0)
+#undef CLV_CASE
+  return hipErrorInvalidValue;
+}
+
+hipError_t persist_occupancy(int D, int K, int* blocks_per_cu) {
+#define CLV_CASE(DD, KK, RR) \
+  if (D == DD && K == KK) return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, persist_kernel<DD, KK>, BLOCK, 0);
+  CLV_FOR_K(CLV_CASE, 2, 0)
+  CLV_FOR_K(CLV_CASE, 3, 0)
 #undef CLV_CASE
   return hipErrorInvalidValue;
 }

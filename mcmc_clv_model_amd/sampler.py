@@ -215,6 +215,13 @@ class HipSampler:
     def synchronize(self) -> None:
         check(self._L.clv_synchronize(self.h))
 
+    def launch_info(self) -> dict:
+        """How clv_run launches (clv_launch_info): persistent kernel or one launch per sweep."""
+        out = (ctypes.c_int64 * 4)()
+        check(self._L.clv_launch_info(self.h, out))
+        return dict(persistent=bool(out[0]), persist_blocks_per_cu=int(out[1]), n_cu=int(out[2]),
+                    workgroups=int(out[3]))
+
     @property
     def sweeps_done(self) -> int:
         return int(self._L.clv_sweeps_done(self.h))

@@ -45,9 +45,9 @@ def main(workload="c2", sweeps=1500, chains=None):
     print(f"    tail: record + counters               {us(st[:, 3] - st[:, 7]):8.2f} us")
     # placement of the latest launch's workgroups: per CU (XCC, SE, CU) count and durations
     nb = -(-s.n // 256)
-    wg = np.zeros(s.chains * nb * 12, np.uint64)
+    wg = np.zeros(s.chains * (nb + 1) * 12, np.uint64)
     assert s._L.clv_debug_wg_stamps(s.h, wg.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))) == 0
-    wg = wg.reshape(-1, 12).astype(np.int64)
+    wg = wg.reshape(-1, 12).astype(np.int64)[:s.chains * nb]
     hw, xcc = wg[:, 2], wg[:, 3] & 0xF
     cu, se = (hw >> 8) & 0xF, (hw >> 13) & 0x7
     key = xcc * 1000 + se * 100 + cu
