@@ -9,9 +9,10 @@ weak scaling: every rank holds one 23,570-customer CDNOW copy of a N x 23,570-cu
 and the ranks exchange the level-2 sufficient statistics once per sweep over RCCL.
 
 Prints ONE JSON line (rank 0).  value = chains * customers * steps / wall time of the timed
-region (hipGraph replay of the fused sweep launches; max over ranks).  roofline: the sweep
-kernel's algorithmic bytes per launch / its mean launch duration, measured with HIP start/stop
-events on every launch of a second timed pass over further sweeps of the same run (per-launch
+region (world size 1: one persistent-kernel launch when the grid fits at once, else hipGraph
+replay of the fused sweep launches; max over ranks).  roofline: the dominant kernel's algorithmic
+bytes per launch / its launch duration, measured with HIP start/stop
+events on the launch(es) of a second timed pass over further sweeps of the same run (per-launch
 events force host-issued launches, so that pass gives kernel durations, not `value`); traffic
 from the committed rocprofv3 PMC summary.  cpu_baseline: the bitwise-pinned numpy restatement of
 the reference (oracle/ref_cpu.py) on 1 core.
@@ -52,7 +53,7 @@ def algorithmic_bytes(D: int, K: int, stored_frac: float, draw_sink: str) -> flo
     return rd + wr + per_store * stored_frac
 
 
-def committed_traffic(workload: str, sharded: bool):
+def committed_traffic(workload: str, sharded: bool, kname: str = "sweep_kernel"):
     """HBM bytes per sweep-kernel launch from the committed rocprofv3 PMC summary of this workload
     (profiles/*_summary.json written by tools/summarize_profile.py): FETCH_SIZE and WRITE_SIZE
     corrected by the calibration kernels of tools/calib_fetch.hip; None if absent."""
@@ -66,8 +67,9 @@ def committed_traffic(workload: str, sharded: bool):
         except Exception:
             continue
         for name, k in d.get("kernels", {}).items():
-            if "sweep_kernel" in name and "traffic_bytes" in k:
-                best = dict(bytes_per_launch=round(k["traffic_bytes"]), source=os.path.basename(path),
+            if kname in name and "traffic_bytes" in k:
+                best = dict(bytes_per_sweep=k["traffic_bytes"] / k.get("sweeps_per_dispatch", 1),
+                            source=os.path.basename(path),
                             counters="FETCH_SIZE x %.2f + WRITE_SIZE x %.2f (calibrated, tools/calib_fetch.hip)"
                                      % (k["traffic_correction"]["read"], k["traffic_correction"]["write"]))
     return best
@@ -76,7 +78,7 @@ def committed_traffic(workload: str, sharded: bool):
 VALU_PEAK_WAVE_INSTS = 1024 * 2.4e9 / 4  # 256 CUs x 4 SIMDs, one wave64 fp64/int64 VALU op per 4 cycles
 
 
-def committed_valu(workload: str, sharded: bool):
+def committed_valu(workload: str, sharded: bool, kname: str = "sweep_kernel"):
     """VALU wave-instructions per sweep-kernel launch (SQ_INSTS_VALU / SQ_WAVES x waves) from the
     committed rocprofv3 summary of this workload; None if absent."""
     import glob
@@ -89,8 +91,9 @@ def committed_valu(workload: str, sharded: bool):
         except Exception:
             continue
         for name, k in d.get("kernels", {}).items():
-            if "sweep_kernel" in name and "valu_insts_per_wave" in k:
-                best = dict(wave_insts_per_launch=k["valu_insts_per_wave"] * k["waves"], source=os.path.basename(path))
+            if kname in name and "valu_insts_per_wave" in k:
+                best = dict(wave_insts_per_sweep=k["valu_insts_per_wave"] * k["waves"] / k.get("sweeps_per_dispatch", 1),
+                            source=os.path.basename(path))
     return best
 
 
@@ -229,6 +232,7 @@ def main():
 
     K = len(covs) + 1
     timing = not a.no_kernel_timing
+    persistent = (not sharded) and kern.launch_info()["persistent"]
     run(a.warmup)
     sync()
     if dist:
@@ -263,22 +267,30 @@ def main():
         kt = kern.kernel_time()
         kern.set_timing(False)
         if kt["sweep_launches"]:
-            t_launch = kt["sweep_ms"] / kt["sweep_launches"] * 1e-3
-            achieved = bpu * chains * n_local / t_launch / 1e9
+            # kt["sweep_launches"] counts sweeps; the persistent kernel runs all n_t in ONE launch
+            t_sweep = kt["sweep_ms"] / kt["sweep_launches"] * 1e-3
+            spl = n_t if persistent else 1               # sweeps per launch
+            t_launch = t_sweep * spl
+            units = chains * n_local * spl               # (chain, customer) sweeps per launch
+            achieved = bpu * units / t_launch / 1e9
+            kname = "persist_kernel" if persistent else "sweep_kernel"
             roofline = dict(bound="hbm", achieved=round(achieved, 3), peak=HBM_PEAK_GBS, unit="GB/s",
                             frac=round(achieved / HBM_PEAK_GBS, 6), traffic=None,
-                            kernel="sweep_kernel (incl. fused level-2 tail)" if not sharded else "sweep_kernel",
-                            bytes_per_unit=round(bpu, 3), units_per_launch=chains * n_local,
-                            sweep_kernel_us=round(t_launch * 1e6, 3), timed_launches=kt["sweep_launches"])
-            tr = committed_traffic(a.workload, sharded)
-            if tr:
-                roofline["traffic"] = tr["bytes_per_launch"]  # HBM bytes per launch (calibrated PMC)
+                            kernel=("persist_kernel (one launch for all sweeps of a clv_run; level-2 workgroup "
+                                    "per chain)") if persistent else
+                            ("sweep_kernel (incl. fused level-2 tail)" if not sharded else "sweep_kernel"),
+                            bytes_per_unit=round(bpu, 3), units_per_launch=units, sweeps_per_launch=spl,
+                            launch_us=round(t_launch * 1e6, 3), sweep_kernel_us=round(t_sweep * 1e6, 3),
+                            timed_launches=kt["sweep_launches"] // spl)
+            tr = committed_traffic(a.workload, sharded, kname)
+            if tr:  # HBM bytes per launch (calibrated PMC), per sweep x sweeps per launch
+                roofline["traffic"] = round(tr["bytes_per_sweep"] * spl)
                 roofline["traffic_source"] = f"{tr['source']}: {tr['counters']}"
             if kt["hyper_launches"]:
                 roofline["hyper_kernel_us"] = round(kt["hyper_ms"] / kt["hyper_launches"] * 1e3, 3)
-            v = committed_valu(a.workload, sharded)
+            v = committed_valu(a.workload, sharded, kname)
             if v:  # the binding resource: VALU issue, not HBM
-                ach = v["wave_insts_per_launch"] / t_launch
+                ach = v["wave_insts_per_sweep"] / t_sweep
                 roofline["valu"] = dict(achieved=round(ach / 1e9, 2), peak=round(VALU_PEAK_WAVE_INSTS / 1e9, 1),
                                         unit="G wave-instructions/s", frac=round(ach / VALU_PEAK_WAVE_INSTS, 4),
                                         source=v["source"],
@@ -301,7 +313,8 @@ def main():
             config=dict(workload=f"{a.workload}: {'bivariate' if D == 2 else 'trivariate'} M2, covariates {covs}",
                         n_customers=n_total, chains=chains, n_mh_steps=20, burnin=burnin, mcmc=mcmc_workload,
                         thin=thin, seed=42, draw_sink=sink, parallelism=f"customer-shard x{world}",
-                        timed_region="hipGraph replay of fused sweep launches" if not sharded else
+                        timed_region=(f"one persistent-kernel launch of {a.steps} sweeps" if persistent else
+                                      "hipGraph replay of fused sweep launches") if not sharded else
                         f"torch.cuda graph replay ({a.graph_chunk} sweeps: sweep + group kernels, RCCL all_gather, "
                         "level-2 kernel)" if a.graph_chunk else "eager: sweep + group kernels, RCCL all_gather, level-2"),
             roofline=roofline, cpu_baseline=cpu,

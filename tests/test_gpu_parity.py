@@ -377,3 +377,50 @@ def test_device_fast_exp_accuracy(L):
     ulp = np.abs(out - ref) / np.spacing(ref)
     assert ulp.max() <= 3.0, ulp.max()
     assert np.mean(out == ref) > 0.6
+
+
+def _run_mode(p, persistent, sweeps, chunks, **kw):
+    """Run `sweeps` sweeps in clv_run calls of `chunks` sizes with the persistent kernel on/off."""
+    from mcmc_clv_model_amd.sampler import HipSampler
+    old = os.environ.get("CLV_PERSISTENT")
+    os.environ["CLV_PERSISTENT"] = "1" if persistent else "0"
+    try:
+        s = HipSampler(p, **kw)
+    finally:
+        if old is None:
+            del os.environ["CLV_PERSISTENT"]
+        else:
+            os.environ["CLV_PERSISTENT"] = old
+    with s:
+        info = s.launch_info()
+        for n in chunks:
+            s.run(n)
+        assert s.sweeps_done == sweeps
+        st = s.get_state()
+        l1, l2, ll = s.read_draws(level1=kw.get("draw_sink", "full") == "full")
+        sums = s.read_summary()[0] if kw.get("draw_sink") == "summary" else None
+    return info, st, l1, l2, ll, sums
+
+
+@pytest.mark.parametrize("D,covs,n,sink", [(2, ["first_sales_scaled"], 23570, "full"),
+                                           (3, ["gender_F", "age_scaled"], 23570, "summary"),
+                                           (2, [], 1000, "full"), (3, ["gender_F"], 300, "full")])
+def test_persistent_kernel_bitwise_equals_launch_per_sweep(L, D, covs, n, sink):
+    """World size 1: the persistent kernel (one launch for all of a clv_run's sweeps, sentinel-slot
+    hand-off to a level-2 workgroup per chain) is chosen by default where the grid fits at once,
+    and reproduces the launch-per-sweep path (fused level-2 tail) bit for bit — state, draws,
+    level-2 records, log-likelihood, summaries — across clv_run calls of uneven length (the
+    carried state at each launch boundary), burn-in and thinning."""
+    df = cdnow("full", n) if n > 2357 else cdnow("abe", n)
+    from mcmc_clv_model_amd.sampler import build_problem
+    p = build_problem(df, covs, D)
+    kw = dict(mcmc=25, burnin=6, thin=3, chains=3, seed=2024, draw_sink=sink)
+    chunks = (1, 7, 2, 20, 1)
+    a = _run_mode(p, True, 31, chunks, **kw)
+    b = _run_mode(p, False, 31, chunks, **kw)
+    assert a[0]["persistent"] and not b[0]["persistent"], (a[0], b[0])
+    for x, y in zip(a[1], b[1]):
+        assert np.array_equal(bits(x), bits(y))
+    for x, y in zip(a[2:], b[2:]):
+        if x is not None:
+            assert np.array_equal(bits(x), bits(y))

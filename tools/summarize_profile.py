@@ -43,13 +43,18 @@ def calibration(prof):
     return out
 
 
-def main(tag, prof=os.path.join(ROOT, "gpurun_out", "prof"), bench_log=None):
+def main(tag, prof=os.path.join(ROOT, "gpurun_out", "prof"), bench_log=None, trace_sweeps=None, pmc_sweeps=None,
+         calib=None):
+    """trace_sweeps: sweeps of each persist_kernel dispatch of the trace pass, in order (the bench's
+    warmup, steps, roofline-pass launches); pmc_sweeps: sweeps of the PMC passes' one persistent
+    dispatch.  The persistent kernel runs many sweeps per launch, so its per-dispatch counters are
+    divided by these to give per-sweep figures (bench.py does the same)."""
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
     stats = list(csv.DictReader(open(os.path.join(prof, "trace", "run_kernel_stats.csv"))))
     shutil.copy(os.path.join(prof, "trace", "run_kernel_stats.csv"), os.path.join(ROOT, "profiles", f"{tag}_kernel_stats.csv"))
     trace = list(csv.DictReader(open(os.path.join(prof, "trace", "run_kernel_trace.csv"))))
     res = {"tag": tag, "kernels": {}}
-    cal = calibration(prof)
+    cal = calibration(calib or prof)
     if cal:
         res["calibration"] = cal
     f_read = cal["FETCH_SIZE"]["read8"] if cal else 2.0   # guide: FETCH_SIZE = 1/2 of the bytes read
@@ -70,6 +75,14 @@ def main(tag, prof=os.path.join(ROOT, "gpurun_out", "prof"), bench_log=None):
             st = [int(t["Start_Timestamp"]) for t in rows]
             en = [int(t["End_Timestamp"]) for t in rows]
             k["median_gap_ns"] = statistics.median([st[i + 1] - en[i] for i in range(len(rows) - 1)])
+        if "persist_kernel" in name:
+            if trace_sweeps and len(trace_sweeps) == len(rows):
+                k["dispatches"] = [dict(sweeps=n, ns=int(t["End_Timestamp"]) - int(t["Start_Timestamp"]),
+                                        ns_per_sweep=(int(t["End_Timestamp"]) - int(t["Start_Timestamp"])) / n)
+                                   for n, t in zip(trace_sweeps, rows)]
+                k["ns_per_sweep"] = sum(d["ns"] for d in k["dispatches"]) / sum(trace_sweeps)
+            if pmc_sweeps:
+                k["sweeps_per_dispatch"] = pmc_sweeps  # of the PMC passes (counters below are per dispatch)
         if name in fetch:
             k["fetch_size_kb"] = fetch[name]
         if name in write:
@@ -78,6 +91,8 @@ def main(tag, prof=os.path.join(ROOT, "gpurun_out", "prof"), bench_log=None):
             k["traffic_bytes_uncorrected"] = (fetch[name] + write[name]) * 1024
             k["traffic_bytes"] = (fetch[name] * f_read + write[name] * f_write) * 1024
             k["traffic_correction"] = dict(read=f_read, write=f_write)
+            if k.get("sweeps_per_dispatch"):
+                k["traffic_bytes_per_sweep"] = k["traffic_bytes"] / k["sweeps_per_dispatch"]
         if name in valu["SQ_WAVES"]:
             waves = valu["SQ_WAVES"][name]
             k["waves"] = waves
@@ -100,4 +115,15 @@ def main(tag, prof=os.path.join(ROOT, "gpurun_out", "prof"), bench_log=None):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], bench_log=os.path.join(ROOT, "gpurun_out", "prof_trace.log"))
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("tag")
+    ap.add_argument("--trace-sweeps", default="", help="comma list: sweeps of each persistent dispatch (trace pass)")
+    ap.add_argument("--pmc-sweeps", type=int, default=0, help="sweeps of the PMC passes' persistent dispatch")
+    ap.add_argument("--prof", default=os.path.join(ROOT, "gpurun_out", "prof"))
+    ap.add_argument("--bench-log", default=os.path.join(ROOT, "gpurun_out", "prof_trace.log"))
+    ap.add_argument("--calib", default=None, help="directory holding calib_FETCH_SIZE/ calib_WRITE_SIZE/")
+    a = ap.parse_args()
+    main(a.tag, prof=a.prof, bench_log=a.bench_log,
+         trace_sweeps=[int(x) for x in a.trace_sweeps.split(",") if x], pmc_sweeps=a.pmc_sweeps or None,
+         calib=a.calib)
