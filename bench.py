@@ -6,7 +6,9 @@ customer.  N=1 workload = BASELINE.json configs[1] ("c2"): bivariate M2 on the f
 (23,570 customers, covariate first_sales_scaled), 4 chains, burnin 10000 / mcmc 10000 / thin 10,
 seed 42, 20 MH steps.  --gpus N > 1 (launched by torch.distributed.run, one rank per GPU) is
 weak scaling: every rank holds one 23,570-customer CDNOW copy of a N x 23,570-customer problem
-and the ranks exchange the level-2 sufficient statistics once per sweep over RCCL.
+and the ranks exchange the level-2 sufficient statistics once per sweep: by default (--exchange
+auto) the persistent kernel of each rank stores its unit partials into every rank's IPC-mapped
+mail over xGMI (after a bitwise check against the RCCL path), else one RCCL all_gather per sweep.
 
 Prints ONE JSON line (rank 0).  value = chains * customers * steps / wall time of the timed
 region (world size 1: one persistent-kernel launch when the grid fits at once, else hipGraph
@@ -179,6 +181,10 @@ def main():
                     help="sharded path: sweeps (incl. the RCCL all-gather) per captured torch.cuda graph; 0 = eager")
     ap.add_argument("--force-sharded", action="store_true",
                     help="use the sharded path (torch.distributed exchange) even at world size 1")
+    ap.add_argument("--exchange", default="auto", choices=["auto", "p2p", "rccl"],
+                    help="world size > 1: unit-partial exchange per sweep — p2p = persistent kernel storing into "
+                         "every rank's IPC-mapped mail over xGMI (auto: where it fits and verifies bitwise "
+                         "against RCCL), rccl = all_gather per sweep")
     ap.add_argument("--cpu-baseline-child", action="store_true")
     ap.add_argument("--cpu-warm", type=int, default=20)
     ap.add_argument("--cpu-timed", type=int, default=200)
@@ -225,14 +231,16 @@ def main():
         from mcmc_clv_model_amd.distributed import ShardedSampler
         p = build_problem(df, covs, D)
         ss = ShardedSampler(p, rank=rank, world=world, chains=chains, mcmc=mcmc, burnin=burnin, thin=thin, seed=42,
-                            draw_sink=sink, device=local_rank, graph_chunk=a.graph_chunk)
+                            draw_sink=sink, device=local_rank, graph_chunk=a.graph_chunk,
+                            exchange=a.exchange if world > 1 else "rccl", verify_sweeps=8)
         run = ss.step
         sync = ss.synchronize
         kern = ss
 
     K = len(covs) + 1
     timing = not a.no_kernel_timing
-    persistent = (not sharded) and kern.launch_info()["persistent"]
+    persistent = kern.launch_info()["persistent"]
+    p2p = sharded and persistent
     run(a.warmup)
     sync()
     if dist:
@@ -277,18 +285,19 @@ def main():
             roofline = dict(bound="hbm", achieved=round(achieved, 3), peak=HBM_PEAK_GBS, unit="GB/s",
                             frac=round(achieved / HBM_PEAK_GBS, 6), traffic=None,
                             kernel=("persist_kernel (one launch for all sweeps of a clv_run; level-2 workgroup "
-                                    "per chain)") if persistent else
+                                    "per chain" + ("; unit partials exchanged over xGMI" if p2p else "") + ")")
+                            if persistent else
                             ("sweep_kernel (incl. fused level-2 tail)" if not sharded else "sweep_kernel"),
                             bytes_per_unit=round(bpu, 3), units_per_launch=units, sweeps_per_launch=spl,
                             launch_us=round(t_launch * 1e6, 3), sweep_kernel_us=round(t_sweep * 1e6, 3),
                             timed_launches=kt["sweep_launches"] // spl)
-            tr = committed_traffic(a.workload, sharded, kname)
+            tr = committed_traffic(a.workload, sharded and not p2p, kname)
             if tr:  # HBM bytes per launch (calibrated PMC), per sweep x sweeps per launch
                 roofline["traffic"] = round(tr["bytes_per_sweep"] * spl)
                 roofline["traffic_source"] = f"{tr['source']}: {tr['counters']}"
             if kt["hyper_launches"]:
                 roofline["hyper_kernel_us"] = round(kt["hyper_ms"] / kt["hyper_launches"] * 1e3, 3)
-            v = committed_valu(a.workload, sharded, kname)
+            v = committed_valu(a.workload, sharded and not p2p, kname)
             if v:  # the binding resource: VALU issue, not HBM
                 ach = v["wave_insts_per_sweep"] / t_sweep
                 roofline["valu"] = dict(achieved=round(ach / 1e9, 2), peak=round(VALU_PEAK_WAVE_INSTS / 1e9, 1),
@@ -315,9 +324,13 @@ def main():
                         thin=thin, seed=42, draw_sink=sink, parallelism=f"customer-shard x{world}",
                         timed_region=(f"one persistent-kernel launch of {a.steps} sweeps" if persistent else
                                       "hipGraph replay of fused sweep launches") if not sharded else
+                        (f"one persistent-kernel launch of {a.steps} sweeps per rank, unit partials stored into "
+                         "every rank's IPC-mapped mail over xGMI (no host collective per sweep)") if p2p else
                         f"torch.cuda graph replay ({a.graph_chunk} sweeps: sweep + group kernels, RCCL all_gather, "
                         "level-2 kernel)" if a.graph_chunk else "eager: sweep + group kernels, RCCL all_gather, level-2"),
             roofline=roofline, cpu_baseline=cpu,
+            exchange=(None if world == 1 and not sharded else
+                      dict(kind=kern.exchange, note=kern.p2p_note, requested=a.exchange if world > 1 else "rccl")),
             speedup_vs_cpu_1core=(value / cpu["value"]) if cpu else None,
         )
         print(json.dumps(line))

@@ -116,7 +116,7 @@ void clv_destroy(clv_sampler* s);
 int clv_set_replay_tape(clv_sampler* s, const double* tape, int64_t n_sweeps);
 int64_t clv_replay_sweep_stride(const clv_sampler* s);
 
-/* Run n sweeps (unsharded: world_size == 1). One sweep = a6's loop body: z (bi:388),
+/* Run n sweeps (world_size == 1, or sharded after clv_p2p_connect). One sweep = a6's loop body: z (bi:388),
  * tau (bi:390), level-2 (bi:393), level-1 MH (bi:396), eta (tri:524-526), storage (bi:402-428).
  * Synchronous; chunks of sweeps are replayed from a captured hipGraph. */
 int clv_run(clv_sampler* s, int64_t n_sweeps);
@@ -139,6 +139,25 @@ int64_t clv_sweeps_done(const clv_sampler* s);
  * workgroups per sweep).  Persistent = one launch for all of a clv_run's sweeps, chosen at create
  * when world_size == 1, Philox mode, every workgroup fits at once, and CLV_PERSISTENT != "0". */
 int clv_launch_info(const clv_sampler* s, int64_t* out);
+/* Sharded runs without a host collective per sweep (world_size > 1, Philox mode): the persistent
+ * kernel's level-2 workgroup of each chain writes this rank's unit partials of sweep s straight into
+ * EVERY rank's mail buffer (device stores over xGMI into IPC-mapped peer memory), waits until its
+ * own mail holds all ranks' units, and sums them in the same global unit order as clv_hyper — so
+ * results are bitwise those of clv_sweep/clv_hyper with an all-gather (and of world size 1).
+ * Replaces, per sweep, the all-gather of bi:243-255's statistics.
+ *   clv_p2p_info:    out[4] = (capable 0/1, connected 0/1, mail bytes, mail device pointer);
+ *                    capable = every workgroup of the persistent grid fits at once on this GPU.
+ *   clv_p2p_export:  this rank's mail buffer as a hipIpcMemHandle (CLV_IPC_HANDLE_BYTES bytes).
+ *   clv_p2p_connect: every rank's mail: handles = [world][CLV_IPC_HANDLE_BYTES] (opened with
+ *                    hipIpcOpenMemHandle; this rank's entry ignored) or ptrs = [world] device
+ *                    pointers valid in this process (ranks sharing one process).  Collective in
+ *                    effect: call it on every rank, then barrier, before the first clv_run.
+ * After connecting, clv_run(n) runs n sweeps (bivariate: after the initial clv_hyper); every rank
+ * must call it with the same n (a rank that waits > 2 s for its peers fails with CLV_EHIP). */
+#define CLV_IPC_HANDLE_BYTES 64
+int clv_p2p_info(const clv_sampler* s, int64_t* out);
+int clv_p2p_export(clv_sampler* s, void* handle);
+int clv_p2p_connect(clv_sampler* s, const void* handles, const uint64_t* ptrs);
 /* Launch on another stream from now on (e.g. a stream under hipGraph capture by the caller,
  * who then replays the captured sweeps), and adjust the host's sweep count by n (+chunk per
  * replay; -chunk after a capture, which records launches without executing them). */

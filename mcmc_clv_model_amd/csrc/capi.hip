@@ -66,6 +66,9 @@ SweepArgs sweep_args(clv_sampler* s, int init, int fuse = 0) {
   a.unitpart = s->d_unit;
   a.hvar_out = s->d_hvar;
   a.stamps = s->d_stamps;
+  a.mail = s->d_mail;
+  a.peers = s->d_peers;
+  a.rank = s->cfg.rank;
   a.h = hyper_args(s, nullptr, 0);
   if (fuse) a.h.hvar = s->replay ? nullptr : s->d_hvar;
   return a;
@@ -326,6 +329,23 @@ int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* pri
     if ((!env || std::string(env) != "0") && (int64_t)s->persist_bpc * s->n_cu >= (int64_t)(nb_local + 1) * C)
       s->persistent = true;
   }
+  // World size > 1: the same persistent kernel exchanging unit partials with its peers over xGMI
+  // (clv_p2p_connect) when the grid fits at once here, as above, and on every rank (the caller
+  // checks that all ranks are capable before connecting).
+  if (!s->replay && cfg->world_size > 1 && nb_local > 0 && nb_local <= 2 * BLOCK && g.n_units_global <= 2 * BLOCK &&
+      bpu <= 64 && (int64_t)g.stride * ((nb_local + bpu - 1) / bpu) <= UMAIL) {
+    hipDeviceProp_t prop{};
+    if (persist_occupancy(g.D, g.K, &s->persist_bpc) == hipSuccess &&
+        hipGetDeviceProperties(&prop, s->device) == hipSuccess)
+      s->n_cu = prop.multiProcessorCount;
+    if ((int64_t)s->persist_bpc * s->n_cu >= (int64_t)(nb_local + 1) * C) {
+      s->p2p_capable = true;
+      const int64_t nm = 2LL * g.world_size * C * g.stride * g.units_per_rank;
+      CLV_HIPC(dalloc(&s->d_mail, nm));
+      CLV_HIPC(hipMemsetAsync(s->d_mail, 0xFF, sizeof(double) * nm, s->stream));  // every slot empty
+      CLV_HIPC(dalloc(&s->d_peers, g.world_size));
+    }
+  }
 #ifdef CLV_STAMPS
   {
     std::vector<unsigned long long> st(1024 * 8 + 12 * (size_t)C * (std::max(nb_local, 1) + 1), 0ull);
@@ -420,6 +440,9 @@ void clv_destroy(clv_sampler* s) {
     if (p) (void)hipFree(p);
   if (s->d_unit && s->d_unit != s->d_block) (void)hipFree(s->d_unit);
   if (s->d_hyp2) (void)hipFree(s->d_hyp2);
+  for (void* p : s->ipc_opened) (void)hipIpcCloseMemHandle(p);
+  if (s->d_mail) (void)hipFree(s->d_mail);
+  if (s->d_peers) (void)hipFree(s->d_peers);
   if (s->own_stream && s->own) (void)hipStreamDestroy(s->own);
   delete s;
 }
@@ -513,6 +536,53 @@ int clv_launch_info(const clv_sampler* s, int64_t* out) {
   return CLV_OK;
 }
 
+int clv_p2p_info(const clv_sampler* s, int64_t* out) {
+  if (!s || !out) return fail(CLV_EINVAL, "null argument");
+  out[0] = s->p2p_capable ? 1 : 0;
+  out[1] = s->p2p_ready ? 1 : 0;
+  out[2] = s->d_mail ? (int64_t)sizeof(double) * 2 * s->g.world_size * s->g.n_chains * s->g.stride * s->g.units_per_rank : 0;
+  out[3] = (int64_t)(uintptr_t)s->d_mail;
+  return CLV_OK;
+}
+
+int clv_p2p_export(clv_sampler* s, void* handle) {
+  if (!s || !handle) return fail(CLV_EINVAL, "null argument");
+  if (!s->p2p_capable) return fail(CLV_ESTATE, "no peer exchange for this geometry (grid does not fit at once)");
+  CLV_HIP(hipSetDevice(s->device));
+  hipIpcMemHandle_t h;
+  CLV_HIP(hipIpcGetMemHandle(&h, s->d_mail));
+  std::memcpy(handle, &h, sizeof(h));
+  return CLV_OK;
+}
+
+int clv_p2p_connect(clv_sampler* s, const void* handles, const uint64_t* ptrs) {
+  if (!s || (!handles && !ptrs)) return fail(CLV_EINVAL, "null argument");
+  if (!s->p2p_capable) return fail(CLV_ESTATE, "no peer exchange for this geometry (grid does not fit at once)");
+  if (s->p2p_ready) return fail(CLV_ESTATE, "already connected");
+  CLV_HIP(hipSetDevice(s->device));
+  const int W = s->g.world_size, r = s->cfg.rank;
+  std::vector<double*> peers(W, nullptr);
+  for (int q = 0; q < W; ++q) {
+    if (q == r) {
+      peers[q] = s->d_mail;
+    } else if (handles) {
+      hipIpcMemHandle_t h;
+      std::memcpy(&h, (const char*)handles + (size_t)q * sizeof(h), sizeof(h));
+      void* p = nullptr;
+      CLV_HIP(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+      s->ipc_opened.push_back(p);
+      peers[q] = (double*)p;
+    } else {
+      peers[q] = (double*)(uintptr_t)ptrs[q];
+    }
+    if (!peers[q]) return fail(CLV_EINVAL, "null peer mail pointer");
+  }
+  CLV_HIP(hipMemcpy(s->d_peers, peers.data(), sizeof(double*) * W, hipMemcpyHostToDevice));
+  CLV_HIP(hipStreamSynchronize(s->stream));  // the mail's sentinel fill (create) has landed
+  s->p2p_ready = true;
+  return CLV_OK;
+}
+
 int clv_set_stream(clv_sampler* s, uint64_t stream) {
   if (!s || !stream) return fail(CLV_EINVAL, "bad arguments");
   if (s->graph_exec) {
@@ -535,7 +605,10 @@ int run_persistent(clv_sampler* s, int64_t n_sweeps) {
   if (n_sweeps == 0) return CLV_OK;
   // every hand-off slot empty (all-ones bytes: the sentinel NaN)
   CLV_HIP(hipMemsetAsync(s->d_hyp2, 0xFF, sizeof(double) * 2 * s->g.n_chains * HS, s->stream));
-  CLV_HIP(hipMemsetAsync(s->d_block, 0xFF, sizeof(double) * s->g.n_chains * s->g.blocks_per_rank * s->g.stride, s->stream));
+  // (only the nb_local live columns of each [chain][stat] row: padding blocks stay 0.0 for the
+  // group kernel of the sharded path)
+  CLV_HIP(hipMemset2DAsync(s->d_block, sizeof(double) * s->g.blocks_per_rank, 0xFF, sizeof(double) * s->g.nb_local,
+                           (size_t)s->g.n_chains * s->g.stride, s->stream));
   SweepArgs a = sweep_args(s, 0, 1);
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (s->timing) {
@@ -557,7 +630,10 @@ int run_persistent(clv_sampler* s, int64_t n_sweeps) {
   CLV_HIP(hipMemcpy(&ab, &s->d_ctrl->abort, sizeof(uint32_t), hipMemcpyDeviceToHost));
   if (ab) {
     (void)hipMemset(&s->d_ctrl->abort, 0, sizeof(uint32_t));
-    return fail(CLV_EHIP, "persistent sweep kernel: a workgroup waited > 2 s for its chain (not all resident?)");
+    if (s->g.world_size > 1) s->p2p_ready = false;  // mail slots are in an unknown state now
+    return fail(CLV_EHIP, s->g.world_size > 1
+                              ? "persistent sweep kernel: a wait exceeded 2 s (a peer rank not running, or not all resident?)"
+                              : "persistent sweep kernel: a workgroup waited > 2 s for its chain (not all resident?)");
   }
   s->sweeps_done += n_sweeps;
   return CLV_OK;
@@ -566,7 +642,13 @@ int run_persistent(clv_sampler* s, int64_t n_sweeps) {
 
 int clv_run(clv_sampler* s, int64_t n_sweeps) {
   if (!s) return fail(CLV_EINVAL, "null sampler");
-  if (s->g.world_size != 1) return fail(CLV_ESTATE, "clv_run is unsharded; use clv_sweep/clv_hyper");
+  if (s->g.world_size != 1) {
+    if (!s->p2p_ready) return fail(CLV_ESTATE, "sharded clv_run needs clv_p2p_connect; else use clv_sweep/clv_hyper");
+    if (s->pending_init_hyper) return fail(CLV_ESTATE, "bivariate: call clv_hyper once before the first sweep");
+    if (n_sweeps < 0) return fail(CLV_EINVAL, "n_sweeps < 0");
+    CLV_HIP(hipSetDevice(s->device));
+    return run_persistent(s, n_sweeps);
+  }
   if (n_sweeps < 0) return fail(CLV_EINVAL, "n_sweeps < 0");
   CLV_HIP(hipSetDevice(s->device));
   int rc = check_replay_range(s, n_sweeps);

@@ -76,6 +76,12 @@ struct clv_sampler {
   double* d_hyp2 = nullptr;         // persistent kernel: [2][chain][HS] hand-off slots
   bool persistent = false;          // clv_run uses persist_kernel (all workgroups resident)
   int persist_bpc = 0, n_cu = 0;    // persist_kernel occupancy (workgroups per CU), CUs
+  // world size > 1: persistent kernel with the peer (xGMI) exchange
+  bool p2p_capable = false;         // the grid fits at once and the unit partials fit UMAIL
+  bool p2p_ready = false;           // clv_p2p_connect done: clv_run runs persist_kernel
+  double* d_mail = nullptr;         // [2][world][chain][stride][units_per_rank]
+  double** d_peers = nullptr;       // [world] mail pointers (peers' opened IPC mappings, own d_mail)
+  std::vector<void*> ipc_opened;    // hipIpcOpenMemHandle mappings to close
   double* d_hvar = nullptr;         // [chain][HV] precomputed hyper variates
   unsigned long long* d_stamps = nullptr;  // CLV_STAMPS diagnostic build only
   double *d_level1 = nullptr, *d_level2 = nullptr, *d_loglik = nullptr, *d_sums = nullptr;

@@ -10,6 +10,8 @@ namespace clv {
 constexpr int BLOCK = CLV_BLOCK;       // customers (lanes) per sweep workgroup
 constexpr int HS = 64;                 // doubles of hyper state per chain
 constexpr int TAPE_HYPER = 40;         // doubles of hyper variates per recorded sweep
+constexpr int UMAIL = 2048;            // persistent kernel, world size > 1: LDS doubles for this rank's
+                                       // unit partials (stride * local units must fit)
 constexpr int HV = 40;                 // precomputed Philox hyper variates per chain: iw normals [0,3),
                                        // chi2 [3,6), beta normals [8,35)
 
@@ -98,6 +100,11 @@ struct SweepArgs {
   double* unitpart;          // [chain][stride][units_per_rank] unit partials (blocks_per_unit > 1)
   double* hvar_out;          // [chain][HV]: the chain's last workgroup precomputes the next level-2
                              // draw's Philox variates at its start (off the critical path), or null
+  // persistent kernel at world size > 1 (peer exchange over xGMI): unit partials of sweep s go
+  // straight into every rank's mail buffer, [2 (sweep parity)][world][chain][stride][units_per_rank]
+  double* mail;              // this rank's mail buffer (device memory, polled by its level-2 workgroups)
+  double* const* peers;      // [world] device pointers to every rank's mail buffer (peers[rank] = mail)
+  int rank;
   HyperArgs h;               // level-2 arguments of the fused tail
   unsigned long long* stamps; // diagnostic build only (CLV_STAMPS): [1024][8] s_memrealtime stamps
 };

@@ -1300,6 +1300,13 @@ __device__ __forceinline__ double ld_wt(const double* p) {
 __device__ __forceinline__ void st_wt(double* p, double v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// System scope for the peer exchange: other GPUs write this rank's mail buffer over xGMI.
+__device__ __forceinline__ double ld_sys(const double* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_sys(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 __device__ __forceinline__ bool slot_full(double v) { return __double_as_longlong(v) != SLOT_EMPTY; }
 __device__ __forceinline__ double slot_empty() { return __longlong_as_double(SLOT_EMPTY); }
 
@@ -1314,6 +1321,213 @@ __device__ __forceinline__ bool wait_expired(uint64_t t0, Ctrl* ctrl, uint32_t p
   return false;
 }
 
+// The chain's level-2 workgroup of persist_kernel (one per chain, grid column nb_local).
+// register arrays (block/unit partials of the chain) do not raise the customer path's pressure.
+template <int D, int K>
+__device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_first, int64_t n_sweeps, int c, uint32_t k0,
+                                            uint32_t k1, int64_t wgi, int64_t it_stamp) {
+  constexpr int NT = BLOCK;
+  constexpr int NXY = K * D;
+  constexpr int NYY = D * (D + 1) / 2;
+  constexpr int NS = NXY + NYY + 1;
+  constexpr int NTRIL = D * (D - 1) / 2;
+  (void)NXY;
+  __shared__ double red[BLOCK / 64][NS];
+  __shared__ double tot[NS];
+  __shared__ double Hs[HS];
+  __shared__ uint32_t s_abort;
+  __shared__ double var_iw[4], var_chi[4], var_noise[32];
+  __shared__ L2Scratch l2;
+  __shared__ double umail[UMAIL];  // world size > 1: this rank's unit partials [stat][local unit]
+  const Geometry& g = a.g;
+  const int tid = threadIdx.x;
+  (void)wgi;
+  double* parts = a.blockpart + (int64_t)c * g.stride * g.blocks_per_rank;  // [stat][block]
+  if (tid == 0) s_abort = 0;
+  __syncthreads();
+  // ================= the chain's level-2 workgroup =================
+  // It shares its CU with customer workgroups; it is on every sweep's critical path, so its
+  // waves take issue priority over theirs (it mostly sleeps in polls otherwise).
+  __builtin_amdgcn_s_setprio(3);
+  stage_prior(a.h.V, &l2);
+  for (int64_t it = 0; it < n_sweeps; ++it) {
+    const int64_t s = s_first + it;
+    const bool stp = tid == 0 && it == it_stamp;
+    (void)stp;
+    const int64_t hs = (D == 2) ? s + 1 : s;  // sweep the drawn (beta, Sigma) belongs to
+    CLV_P_STAMP(a.stamps, wgi, 0, stp);
+    // 1. this draw's variates (as hyper_body without precomputed ones): overlap the sweep
+    if (tid < NTRIL) var_iw[tid] = hyper_normal(k0, k1, HSLOT_NORMAL0 + tid, (uint32_t)hs);
+    if (tid >= 32 && tid < 32 + D * K) var_noise[tid - 32] = hyper_normal(k0, k1, HSLOT_BETA_NORMAL0 + (tid - 32), (uint32_t)hs);
+    if (tid >= 64 && tid < 64 + D) var_chi[tid - 64] = chi2_draw(k0, k1, (uint32_t)hs, tid - 64, a.h.nu_n - D + 1 + (tid - 64));
+    __syncthreads();
+    if (tid == 0) bartlett_inverse<D>(var_iw, var_chi, l2.Ai);  // read back by this lane only
+    CLV_P_STAMP(a.stamps, wgi, 1, stp);
+    // 2. wait for every block partial of sweep s (lane tid: blocks tid, tid + NT, ...; nb <= 2 NT)
+    double v0[NS], v1[NS];
+    const int b0 = tid, b1 = tid + NT;
+    {  // each wavefront polls on its own (no barrier per poll); a lane stops once its slots are full
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      bool done = false;
+      for (uint32_t poll = 0;; ++poll) {
+        if (!done) {
+          bool ok = true;
+#pragma unroll
+          for (int j = 0; j < NS; ++j) {
+            v0[j] = b0 < g.nb_local ? ld_wt(parts + (int64_t)j * g.blocks_per_rank + b0) : 0.0;
+            v1[j] = b1 < g.nb_local ? ld_wt(parts + (int64_t)j * g.blocks_per_rank + b1) : 0.0;
+          }
+#pragma unroll
+          for (int j = 0; j < NS; ++j) ok = ok && slot_full(v0[j]) && slot_full(v1[j]);
+          done = ok;
+        }
+        if (__all(done)) break;
+        if (wait_expired(t0, a.ctrl_rw, poll)) {
+          s_abort = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    __syncthreads();
+    if (s_abort) return;
+    CLV_P_STAMP(a.stamps, wgi, 2, stp);
+    // 3. the fused path's fixed-order sum (hyper_body: lane u sums units u, u + NT, ... in order)
+    double acc[NS];
+    const int64_t per_rank = (int64_t)g.n_chains * NS * g.units_per_rank;  // mail doubles per rank and parity
+    const double* mb = a.mail + (int64_t)(s & 1) * g.world_size * per_rank + (int64_t)c * NS * g.units_per_rank;
+    const int64_t u0 = tid, u1 = tid + NT;  // global units this lane sums (n_units_global <= 2 NT)
+    if (g.world_size == 1) {
+#pragma unroll
+      for (int j = 0; j < NS; ++j) {
+        acc[j] = 0.0;
+        if (b0 < g.nb_local) acc[j] += v0[j];
+        if (b1 < g.nb_local) acc[j] += v1[j];
+      }
+    } else {
+      // 3a. this rank's unit partials: blocks_per_unit consecutive blocks summed in group_kernel's
+      //     order (a unit's blocks sit in consecutive lanes of one wavefront: bpu | 64)
+      const int bpu = g.blocks_per_unit;
+      const int ul = (g.nb_local + bpu - 1) / bpu;
+      const int lane = tid & 63;
+#pragma unroll
+      for (int j = 0; j < NS; ++j) {
+        double t0 = 0.0, t1 = 0.0;
+        for (int k = 0; k < bpu; ++k) {
+          t0 += __shfl(v0[j], lane + k, 64);  // blocks >= nb_local contribute 0.0, as group_kernel's
+          t1 += __shfl(v1[j], lane + k, 64);  // zero-initialised padding blocks do
+        }
+        if (tid % bpu == 0) {
+          if (tid / bpu < ul) umail[j * ul + tid / bpu] = t0;
+          if ((tid + NT) / bpu < ul) umail[j * ul + (tid + NT) / bpu] = t1;
+        }
+      }
+      __syncthreads();
+      // 3b. to every rank's mail slot of sweep s (write-through stores over xGMI; the value is
+      //     its own arrival flag — the sentinel never occurs in a partial)
+      const int64_t dst = ((int64_t)(s & 1) * g.world_size + a.rank) * per_rank + (int64_t)c * NS * g.units_per_rank;
+      for (int e = tid; e < NS * ul; e += NT) {
+        const int j = e / ul, lu = e - j * ul;
+        const double v = umail[e];
+        for (int q = 0; q < g.world_size; ++q) st_sys(a.peers[q] + dst + (int64_t)j * g.units_per_rank + lu, v);
+      }
+      // 3c. wait for every rank's units in this rank's mail, then the fixed-order sum
+      double w0[NS], w1[NS];
+      const double* p0 = mb + (u0 / g.units_per_rank) * per_rank + (u0 % g.units_per_rank);
+      const double* p1 = mb + (u1 / g.units_per_rank) * per_rank + (u1 % g.units_per_rank);
+      const bool h0 = u0 < g.n_units_global, h1 = u1 < g.n_units_global;
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      bool done = false;
+      for (uint32_t poll = 0;; ++poll) {
+        if (!done) {
+          bool ok = true;
+#pragma unroll
+          for (int j = 0; j < NS; ++j) {
+            w0[j] = h0 ? ld_sys(p0 + (int64_t)j * g.units_per_rank) : 0.0;
+            w1[j] = h1 ? ld_sys(p1 + (int64_t)j * g.units_per_rank) : 0.0;
+          }
+#pragma unroll
+          for (int j = 0; j < NS; ++j) ok = ok && slot_full(w0[j]) && slot_full(w1[j]);
+          done = ok;
+        }
+        if (__all(done)) break;
+        if (wait_expired(t0, a.ctrl_rw, poll)) {
+          s_abort = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      __syncthreads();
+      if (s_abort) return;
+#pragma unroll
+      for (int j = 0; j < NS; ++j) {
+        acc[j] = 0.0;
+        if (h0) acc[j] += w0[j];
+        if (h1) acc[j] += w1[j];
+      }
+#pragma unroll
+      for (int j = 0; j < NS; ++j) {  // empty again before any rank can write sweep s + 2 here
+        if (h0) st_sys((double*)p0 + (int64_t)j * g.units_per_rank, slot_empty());
+        if (h1) st_sys((double*)p1 + (int64_t)j * g.units_per_rank, slot_empty());
+      }
+    }
+    block_reduce<NS, NT>(acc, red, tot);  // also publishes the variates (LDS)
+    CLV_P_STAMP(a.stamps, wgi, 6, stp);
+    // 4. reset: the partial slots (their writers write again only after step 6) and the
+    //    (beta, Sigma) set every reader of s has read (its next write is for s+2)
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+      if (b0 < g.nb_local) st_wt(parts + (int64_t)j * g.blocks_per_rank + b0, slot_empty());
+      if (b1 < g.nb_local) st_wt(parts + (int64_t)j * g.blocks_per_rank + b1, slot_empty());
+    }
+    if (it > 0 && tid < HS) st_wt(a.hyp2 + ((int64_t)(s & 1) * g.n_chains + c) * HS + tid, slot_empty());
+    if (tid < HS) Hs[tid] = 0.0;  // unwritten hyper slots publish as 0 (wavefront 0: ordered before the draw's writes)
+    // 5. the draw (wavefront 0) while the resets drain
+    level2_draw<D, K>(tot, var_iw, var_chi, var_noise, false, &l2, l2.Ai);
+    CLV_P_STAMP(a.stamps, wgi, 7, stp);
+    if (tid == 0) {
+      double Sig[D][D];
+#pragma unroll
+      for (int p = 0; p < D; ++p)
+#pragma unroll
+        for (int q = 0; q < D; ++q) Sig[p][q] = l2.Sig[p * D + q];
+      finalize_hyper<D, K, true>(l2.beta, Sig, a.h.omega2, Hs);
+    }
+    CLV_P_STAMP(a.stamps, wgi, 3, stp);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // resets landed (each wave its own)
+    __syncthreads();
+    // 6. publish (beta, Sigma) of sweep s+1: one coalesced write-through store per lane
+    const bool last = it == n_sweeps - 1;
+    if (tid < HS) {
+      if (last) a.h.hyper[(int64_t)c * HS + tid] = Hs[tid];  // the carried state (kernel boundary)
+      else st_wt(a.hyp2 + ((int64_t)((s + 1) & 1) * g.n_chains + c) * HS + tid, Hs[tid]);
+    }
+    CLV_P_STAMP(a.stamps, wgi, 4, stp);
+    CLV_P_STAMP(a.stamps, wgi, 5, tid == 0 && it + 1 == it_stamp);  // the previous sweep's publish
+#ifdef CLV_STAMPS
+    if (tid == 0 && a.stamps && c < 8 && it % 4 == 0 && it / 4 < 1024)  // publish times, every 4th sweep
+      a.stamps[(it / 4) * 8 + c] = __builtin_amdgcn_s_memrealtime();
+#endif
+    // 7. records (off the critical path)
+    const bool store_l2 = hs >= 1 && is_stored(hs, g);
+    double* o = store_l2 ? a.h.level2 + ((int64_t)c * g.n_draws + draw_index(hs, g)) * g.l2w : nullptr;
+    if (tid < K * D && store_l2) o[(tid % D) * K + tid / D] = l2.beta[tid];  // beta.T.ravel() (bi:411)
+    if (tid == 0) {
+      if (store_l2) {
+        int q = K * D;
+#pragma unroll
+        for (int p = 0; p < D; ++p)
+#pragma unroll
+          for (int r = p; r < D; ++r) o[q++] = l2.Sig[p * D + r];  // bi:412, tri:550-554
+      }
+      if (is_stored(s, g)) a.h.loglik[(int64_t)c * g.n_draws + draw_index(s, g)] = tot[NS - 1] / (double)g.n_global;
+      if (last) a.ctrl_rw->cur = s;
+    }
+    __syncthreads();  // LDS (tot, l2, Hs, variates) reused next sweep
+  }
+  return;
+}
+
 template <int D, int K>
 __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t s_first, int64_t n_sweeps) {
   constexpr int NT = BLOCK;
@@ -1326,8 +1540,6 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
   __shared__ double exp_tab[EXP_TAB_N];
   __shared__ double Hs[HS];
   __shared__ uint32_t s_abort;
-  __shared__ double var_iw[4], var_chi[4], var_noise[32];
-  __shared__ L2Scratch l2;
   const Geometry& g = a.g;
   const int c = blockIdx.y;
   const int b = blockIdx.x;
@@ -1341,116 +1553,8 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
   double* parts = a.blockpart + (int64_t)c * g.stride * g.blocks_per_rank;  // [stat][block]
   if (tid == 0) s_abort = 0;
 
-  if (b == g.nb_local) {
-    // ================= the chain's level-2 workgroup =================
-    // It shares its CU with customer workgroups; it is on every sweep's critical path, so its
-    // waves take issue priority over theirs (it mostly sleeps in polls otherwise).
-    __builtin_amdgcn_s_setprio(3);
-    stage_prior(a.h.V, &l2);
-    for (int64_t it = 0; it < n_sweeps; ++it) {
-      const int64_t s = s_first + it;
-      const bool stp = tid == 0 && it == it_stamp;
-      (void)stp;
-      const int64_t hs = (D == 2) ? s + 1 : s;  // sweep the drawn (beta, Sigma) belongs to
-      CLV_P_STAMP(a.stamps, wgi, 0, stp);
-      // 1. this draw's variates (as hyper_body without precomputed ones): overlap the sweep
-      if (tid < NTRIL) var_iw[tid] = hyper_normal(k0, k1, HSLOT_NORMAL0 + tid, (uint32_t)hs);
-      if (tid >= 32 && tid < 32 + D * K) var_noise[tid - 32] = hyper_normal(k0, k1, HSLOT_BETA_NORMAL0 + (tid - 32), (uint32_t)hs);
-      if (tid >= 64 && tid < 64 + D) var_chi[tid - 64] = chi2_draw(k0, k1, (uint32_t)hs, tid - 64, a.h.nu_n - D + 1 + (tid - 64));
-      __syncthreads();
-      if (tid == 0) bartlett_inverse<D>(var_iw, var_chi, l2.Ai);  // read back by this lane only
-      CLV_P_STAMP(a.stamps, wgi, 1, stp);
-      // 2. wait for every block partial of sweep s (lane tid: blocks tid, tid + NT, ...; nb <= 2 NT)
-      double v0[NS], v1[NS];
-      const int b0 = tid, b1 = tid + NT;
-      {  // each wavefront polls on its own (no barrier per poll); a lane stops once its slots are full
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        bool done = false;
-        for (uint32_t poll = 0;; ++poll) {
-          if (!done) {
-            bool ok = true;
-#pragma unroll
-            for (int j = 0; j < NS; ++j) {
-              v0[j] = b0 < g.nb_local ? ld_wt(parts + (int64_t)j * g.blocks_per_rank + b0) : 0.0;
-              v1[j] = b1 < g.nb_local ? ld_wt(parts + (int64_t)j * g.blocks_per_rank + b1) : 0.0;
-            }
-#pragma unroll
-            for (int j = 0; j < NS; ++j) ok = ok && slot_full(v0[j]) && slot_full(v1[j]);
-            done = ok;
-          }
-          if (__all(done)) break;
-          if (wait_expired(t0, a.ctrl_rw, poll)) {
-            s_abort = 1;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-        }
-      }
-      __syncthreads();
-      if (s_abort) return;
-      CLV_P_STAMP(a.stamps, wgi, 2, stp);
-      // 3. the fused path's fixed-order sum (hyper_body: lane u sums units u, u + NT, ... in order)
-      double acc[NS];
-#pragma unroll
-      for (int j = 0; j < NS; ++j) {
-        acc[j] = 0.0;
-        if (b0 < g.nb_local) acc[j] += v0[j];
-        if (b1 < g.nb_local) acc[j] += v1[j];
-      }
-      block_reduce<NS, NT>(acc, red, tot);  // also publishes the variates (LDS)
-      CLV_P_STAMP(a.stamps, wgi, 6, stp);
-      // 4. reset: the partial slots (their writers write again only after step 6) and the
-      //    (beta, Sigma) set every reader of s has read (its next write is for s+2)
-#pragma unroll
-      for (int j = 0; j < NS; ++j) {
-        if (b0 < g.nb_local) st_wt(parts + (int64_t)j * g.blocks_per_rank + b0, slot_empty());
-        if (b1 < g.nb_local) st_wt(parts + (int64_t)j * g.blocks_per_rank + b1, slot_empty());
-      }
-      if (it > 0 && tid < HS) st_wt(a.hyp2 + ((int64_t)(s & 1) * g.n_chains + c) * HS + tid, slot_empty());
-      if (tid < HS) Hs[tid] = 0.0;  // unwritten hyper slots publish as 0 (wavefront 0: ordered before the draw's writes)
-      // 5. the draw (wavefront 0) while the resets drain
-      level2_draw<D, K>(tot, var_iw, var_chi, var_noise, false, &l2, l2.Ai);
-      CLV_P_STAMP(a.stamps, wgi, 7, stp);
-      if (tid == 0) {
-        double Sig[D][D];
-#pragma unroll
-        for (int p = 0; p < D; ++p)
-#pragma unroll
-          for (int q = 0; q < D; ++q) Sig[p][q] = l2.Sig[p * D + q];
-        finalize_hyper<D, K, true>(l2.beta, Sig, a.h.omega2, Hs);
-      }
-      CLV_P_STAMP(a.stamps, wgi, 3, stp);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // resets landed (each wave its own)
-      __syncthreads();
-      // 6. publish (beta, Sigma) of sweep s+1: one coalesced write-through store per lane
-      const bool last = it == n_sweeps - 1;
-      if (tid < HS) {
-        if (last) a.h.hyper[(int64_t)c * HS + tid] = Hs[tid];  // the carried state (kernel boundary)
-        else st_wt(a.hyp2 + ((int64_t)((s + 1) & 1) * g.n_chains + c) * HS + tid, Hs[tid]);
-      }
-      CLV_P_STAMP(a.stamps, wgi, 4, stp);
-      CLV_P_STAMP(a.stamps, wgi, 5, tid == 0 && it + 1 == it_stamp);  // the previous sweep's publish
-#ifdef CLV_STAMPS
-      if (tid == 0 && a.stamps && c < 8 && it % 4 == 0 && it / 4 < 1024)  // publish times, every 4th sweep
-        a.stamps[(it / 4) * 8 + c] = __builtin_amdgcn_s_memrealtime();
-#endif
-      // 7. records (off the critical path)
-      const bool store_l2 = hs >= 1 && is_stored(hs, g);
-      double* o = store_l2 ? a.h.level2 + ((int64_t)c * g.n_draws + draw_index(hs, g)) * g.l2w : nullptr;
-      if (tid < K * D && store_l2) o[(tid % D) * K + tid / D] = l2.beta[tid];  // beta.T.ravel() (bi:411)
-      if (tid == 0) {
-        if (store_l2) {
-          int q = K * D;
-#pragma unroll
-          for (int p = 0; p < D; ++p)
-#pragma unroll
-            for (int r = p; r < D; ++r) o[q++] = l2.Sig[p * D + r];  // bi:412, tri:550-554
-        }
-        if (is_stored(s, g)) a.h.loglik[(int64_t)c * g.n_draws + draw_index(s, g)] = tot[NS - 1] / (double)g.n_global;
-        if (last) a.ctrl_rw->cur = s;
-      }
-      __syncthreads();  // LDS (tot, l2, Hs, variates) reused next sweep
-    }
+  if (b == g.nb_local) {  // the chain's level-2 workgroup
+    persist_level2<D, K>(a, s_first, n_sweeps, c, k0, k1, wgi, it_stamp);
     return;
   }
 

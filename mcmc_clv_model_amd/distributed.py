@@ -9,6 +9,12 @@ assembles [world][chain][stride][units_per_rank], and every rank performs the id
 fixed-order sum and the identical level-2 draw (same Philox counter), so no broadcast is needed
 and results are bitwise independent of the GPU count.
 
+``exchange="p2p"`` (or "auto": p2p where possible and verified, else RCCL) replaces the host
+collective per sweep: the ranks swap hipIpcMemHandles of their mail buffers once, and the
+persistent sweep kernel's level-2 workgroup of each chain stores its rank's unit partials
+straight into every rank's mail over xGMI, waits for all ranks' units in its own mail and sums
+them in the same global order — one kernel launch per step per rank, same bits as RCCL.
+
 Shard plan (a function of n_global and world only):
   blocks_per_unit G  = clv_default_blocks_per_unit(n_global)     (units <= 512)
   blocks_per_rank    = ceil(ceil(n_blocks / world) / G) * G
@@ -78,8 +84,15 @@ def slice_problem(p, begin: int, end: int):
 
 
 def exchange(local, gathered, group=None) -> None:
-    """All-gather this rank's unit partials (1-D tensor) into ``gathered`` (world * len)."""
+    """All-gather this rank's unit partials (1-D tensor) into ``gathered`` (world * len).
+    A "gloo" group (tests: several ranks sharing one GPU, which RCCL refuses) goes through host
+    copies."""
     import torch.distributed as dist
+    if local.is_cuda and dist.get_backend(group) == "gloo":
+        h = gathered.new_empty(gathered.shape, device="cpu")
+        dist.all_gather_into_tensor(h, local.cpu(), group=group)
+        gathered.copy_(h)
+        return
     dist.all_gather_into_tensor(gathered, local, group=group)
 
 
@@ -102,7 +115,7 @@ class ShardedSampler:
 
     def __init__(self, p_global, *, rank: int, world: int, chains: int, mcmc: int, burnin: int, thin: int,
                  seed: int, n_mh_steps: int = 20, draw_sink: str = "summary", device: int = 0, group=None,
-                 graph_chunk: int = 0):
+                 graph_chunk: int = 0, exchange: str = "rccl", verify_sweeps: int = 8):
         import torch
         from .sampler import HipSampler, make_prior
         self.torch = torch
@@ -132,6 +145,76 @@ class ShardedSampler:
         self.D = p_global.D
         if self.D == 2:  # bivariate: the draw for sweep 1 comes from the initial state (bi:393)
             self._exchange_and_hyper()
+        if exchange not in ("rccl", "p2p", "auto"):
+            raise ValueError("exchange must be 'rccl', 'p2p' or 'auto'")
+        self.exchange = "rccl"
+        self.p2p_note = None
+        if exchange != "rccl" and world > 1:
+            self._setup_p2p(required=exchange == "p2p", verify_sweeps=int(verify_sweeps))
+
+    # ---- peer exchange: the persistent kernel writes unit partials into every rank's mail over xGMI
+    def _all_ok(self, ok: bool) -> bool:
+        """True iff ``ok`` on every rank (MIN all-reduce over the process group)."""
+        import torch.distributed as dist
+        dev = "cpu" if dist.get_backend(self.group) == "gloo" else self.gathered.device
+        t = self.torch.tensor([1 if ok else 0], dtype=self.torch.int32, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
+        return bool(t.item())
+
+    def _setup_p2p(self, required: bool, verify_sweeps: int) -> None:
+        """Connect the ranks' mail buffers (hipIpcMemHandle exchange over the process group) so
+        that clv_run runs all sweeps of a step in ONE persistent launch per rank, with no host
+        collective per sweep.  ``verify_sweeps`` > 0 (burn-in sweeps only) first runs that many
+        sweeps through the RCCL path and, from the same state, through the peer path, and keeps
+        the peer path only if every rank's state is bitwise identical (else RCCL, or an error
+        when ``required``)."""
+        import torch.distributed as dist
+        capable = self._all_ok(self.s.p2p_info()["capable"])
+        if not capable:
+            if required:
+                raise _lib.ClvError("p2p exchange: the persistent grid does not fit at once on every rank")
+            self.p2p_note = "not capable (grid does not fit at once on every rank)"
+            return
+        handles = [None] * self.world
+        dist.all_gather_object(handles, self.s.p2p_export(), group=self.group)
+        err = None
+        try:
+            self.s.p2p_connect(handles=handles)
+        except Exception as e:  # noqa: BLE001 - reported below, on every rank
+            err = e
+        if not self._all_ok(err is None):
+            if required:
+                raise _lib.ClvError(f"p2p exchange: connect failed ({err})")
+            self.p2p_note = f"connect failed ({err})"
+            return
+        dist.barrier(group=self.group)
+        if verify_sweeps > 0:
+            n0 = self.s.sweeps_done
+            if n0 + verify_sweeps > self.s.burnin:
+                raise ValueError("verify_sweeps must fit in the burn-in (nothing may be stored twice)")
+            snap = self.s.get_state()
+            self._eager(verify_sweeps)
+            self.synchronize()
+            ref = self.s.get_state()
+            self.s.set_state(*snap, n0)
+            dist.barrier(group=self.group)
+            err = None
+            try:
+                self.s.run(verify_sweeps)
+                got = self.s.get_state()
+                same = all(np.array_equal(a.view(np.uint64), b.view(np.uint64)) for a, b in zip(ref, got))
+            except Exception as e:  # noqa: BLE001
+                same, err = False, e
+            if not self._all_ok(same):
+                self.s.set_state(*snap, n0)  # the RCCL path carries on from the same state
+                if required:
+                    raise _lib.ClvError(f"p2p exchange: verification against RCCL failed ({err or 'state differs'})")
+                self.p2p_note = f"verification against RCCL failed ({err or 'state differs'})"
+                return
+            self.s.set_state(*snap, n0)
+            dist.barrier(group=self.group)
+        self.exchange = "p2p"
+        self.p2p_note = f"verified bitwise against RCCL over {verify_sweeps} sweeps" if verify_sweeps > 0 else None
 
     def _exchange_and_hyper(self) -> None:
         with self.torch.cuda.stream(self.cur):
@@ -145,6 +228,9 @@ class ShardedSampler:
 
     def step(self, n: int = 1) -> None:
         torch = self.torch
+        if self.exchange == "p2p":  # one persistent launch per rank; every rank calls with the same n
+            self.s.run(n)
+            return
         left = n
         if self.graph_chunk and not self.timing:
             if self.graph is None and left >= self.graph_chunk:
@@ -172,6 +258,12 @@ class ShardedSampler:
         self.s.note_sweeps(-self.graph_chunk)  # capture recorded the launches, it ran nothing
         self.graph = g
         torch.cuda.synchronize()
+
+    def launch_info(self) -> dict:
+        """clv_launch_info, with ``persistent`` = this rank runs whole steps in one launch (p2p)."""
+        info = self.s.launch_info()
+        info["persistent"] = self.exchange == "p2p"
+        return info
 
     def set_timing(self, enable: bool) -> None:
         self.timing = bool(enable)

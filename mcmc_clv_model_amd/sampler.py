@@ -222,6 +222,29 @@ class HipSampler:
         return dict(persistent=bool(out[0]), persist_blocks_per_cu=int(out[1]), n_cu=int(out[2]),
                     workgroups=int(out[3]))
 
+    # ---- peer exchange (world size > 1 through the persistent kernel, include/clvmcmc.h)
+    IPC_HANDLE_BYTES = 64
+
+    def p2p_info(self) -> dict:
+        out = (ctypes.c_int64 * 4)()
+        check(self._L.clv_p2p_info(self.h, out))
+        return dict(capable=bool(out[0]), connected=bool(out[1]), mail_bytes=int(out[2]), mail_ptr=int(out[3]))
+
+    def p2p_export(self) -> bytes:
+        """This rank's mail buffer as a hipIpcMemHandle (bytes) for the other ranks."""
+        buf = ctypes.create_string_buffer(self.IPC_HANDLE_BYTES)
+        check(self._L.clv_p2p_export(self.h, buf))
+        return buf.raw
+
+    def p2p_connect(self, handles: Optional[Sequence[bytes]] = None, ptrs: Optional[Sequence[int]] = None) -> None:
+        """Every rank's mail: IPC handles (one process per GPU) or device pointers (one process)."""
+        if handles is not None:
+            blob = ctypes.create_string_buffer(b"".join(handles), self.IPC_HANDLE_BYTES * len(handles))
+            check(self._L.clv_p2p_connect(self.h, blob, None))
+        else:
+            arr = (ctypes.c_uint64 * len(ptrs))(*[int(p) for p in ptrs])
+            check(self._L.clv_p2p_connect(self.h, None, arr))
+
     @property
     def sweeps_done(self) -> int:
         return int(self._L.clv_sweeps_done(self.h))

@@ -1,0 +1,169 @@
+"""Row (e), peer exchange: the persistent sweep kernel at world size > 1 (clv_p2p_connect,
+include/clvmcmc.h) — each chain's level-2 workgroup stores its rank's unit partials straight into
+every rank's mail buffer and sums all ranks' units in the global fixed order — reproduces the
+unsharded run bit for bit (state, level-2 records, log-likelihood, summaries).
+
+On the one-GPU test box the "ranks" share the card: in one process (mail pointers, one host
+thread per rank, since every rank's launch must be resident at once) and in two processes
+(hipIpcMemHandle exchange over a gloo group, through ShardedSampler(exchange="p2p") incl. its
+bitwise verification against the all-gather path)."""
+import os
+import socket
+import subprocess
+import sys
+import threading
+
+import numpy as np
+import pytest
+
+from tests.helpers import bits, cdnow
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _ref_run(p, sweeps, kw):
+    from mcmc_clv_model_amd.sampler import HipSampler
+    with HipSampler(p, **kw) as s:
+        s.run(sweeps)
+        st = s.get_state()
+        sums = s.read_summary()[0] if kw["draw_sink"] == "summary" else None
+        l1, l2, ll = s.read_draws(level1=kw["draw_sink"] == "full")
+    return st, sums, l1, l2, ll
+
+
+@pytest.mark.parametrize("D,covs,n,world,sink", [(2, ["first_sales_scaled"], 23570, 2, "summary"),
+                                                 (3, ["gender_F", "age_scaled"], 23570, 3, "full"),
+                                                 (2, [], 2357, 2, "full")])
+def test_p2p_persistent_bitwise_equals_unsharded(D, covs, n, world, sink):
+    import torch
+    from mcmc_clv_model_amd import distributed as Dm
+    from mcmc_clv_model_amd.sampler import HipSampler, build_problem, make_prior
+    df = cdnow("full", n) if n > 2357 else cdnow("abe", n)
+    p = build_problem(df, covs, D)
+    kw = dict(mcmc=9, burnin=4, thin=2, chains=2, seed=4242, draw_sink=sink)
+    chunks = (1, 5, 7)
+    sweeps = sum(chunks)
+    ref, ref_sums, ref_l1, ref_l2, ref_ll = _ref_run(p, sweeps, kw)
+
+    plan = Dm.plan(p.N, world)
+    prior = make_prior(p, p.N)
+    shards = []
+    for r in range(world):
+        b, e = plan.shard(r)
+        shards.append(HipSampler(Dm.slice_problem(p, b, e), n_global=p.N, shard_begin=r * plan.blocks_per_rank * 256,
+                                 world_size=world, rank=r, blocks_per_rank=plan.blocks_per_rank,
+                                 blocks_per_unit=plan.blocks_per_unit, prior=prior, **kw))
+    try:
+        info = [sh.p2p_info() for sh in shards]
+        assert all(i["capable"] and not i["connected"] for i in info), info
+        with pytest.raises(Exception, match="clv_p2p_connect"):
+            shards[0].run(1)  # sharded clv_run needs the connection
+        if D == 2:  # bivariate: the initial draw from the initial state, through the all-gather path
+            nd = shards[0].partials()[1]
+            gathered = torch.zeros(nd * world, dtype=torch.float64, device="cuda")
+            for r, sh in enumerate(shards):
+                sh.copy_partials(gathered.data_ptr() + r * nd * 8)
+                sh.synchronize()
+            for sh in shards:
+                sh.hyper(gathered.data_ptr())
+                sh.synchronize()
+        ptrs = [i["mail_ptr"] for i in info]
+        for sh in shards:
+            sh.p2p_connect(ptrs=ptrs)
+        assert all(sh.p2p_info()["connected"] for sh in shards)
+
+        for n_run in chunks:  # every rank's launch runs at once (one host thread each)
+            errs = []
+
+            def go(sh):
+                try:
+                    sh.run(n_run)
+                except Exception as e:  # noqa: BLE001
+                    errs.append(e)
+
+            th = [threading.Thread(target=go, args=(sh,)) for sh in shards]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join(timeout=60)
+            assert not any(t.is_alive() for t in th)
+            assert not errs, errs
+        for r, sh in enumerate(shards):
+            b, e = plan.shard(r)
+            assert sh.sweeps_done == sweeps
+            lam, mu, beta, sigma = sh.get_state()
+            assert np.array_equal(bits(lam), bits(ref[0][:, b:e])) and np.array_equal(bits(mu), bits(ref[1][:, b:e]))
+            assert np.array_equal(bits(beta), bits(ref[2])) and np.array_equal(bits(sigma), bits(ref[3]))
+            l1, l2, ll = sh.read_draws(level1=sink == "full")
+            assert np.array_equal(bits(l2), bits(ref_l2)) and np.array_equal(bits(ll), bits(ref_ll))
+            if sink == "full":
+                assert np.array_equal(bits(l1), bits(ref_l1[:, :, b:e]))
+            else:
+                assert np.array_equal(bits(sh.read_summary()[0]), bits(ref_sums[:, :, b:e]))
+    finally:
+        for sh in shards:
+            sh.close()
+
+
+WORKER = r"""
+import json, os, sys
+sys.path.insert(0, os.environ["CLV_ROOT"])
+import numpy as np
+import torch.distributed as dist
+from tests.helpers import bits, cdnow
+from mcmc_clv_model_amd.sampler import HipSampler, build_problem
+from mcmc_clv_model_amd.distributed import ShardedSampler
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+D = int(os.environ["CLV_D"])
+covs = ["first_sales_scaled"] if D == 2 else ["gender_F", "age_scaled"]
+p = build_problem(cdnow("full", 12000), covs, D)
+kw = dict(mcmc=6, burnin=12, thin=2, chains=2, seed=7, draw_sink="summary")
+with HipSampler(p, **kw) as s:          # unsharded reference, before any rank's persistent launch
+    s.run(17)
+    ref = s.get_state()
+    ref_sums = s.read_summary()[0]
+dist.init_process_group("gloo")
+ss = ShardedSampler(p, rank=rank, world=world, device=0, exchange="p2p", verify_sweeps=4, **kw)
+ss.step(9)
+ss.step(8)
+ss.synchronize()
+b, e = ss.begin, ss.end
+got = ss.s.get_state()
+ok = (ss.exchange == "p2p" and ss.s.sweeps_done == 17
+      and all(np.array_equal(bits(x), bits(y[:, b:e] if i < 2 else y)) for i, (x, y) in enumerate(zip(got, ref)))
+      and np.array_equal(bits(ss.s.read_summary()[0]), bits(ref_sums[:, :, b:e])))
+print(json.dumps(dict(rank=rank, ok=bool(ok), note=ss.p2p_note)), flush=True)
+ss.close()
+dist.destroy_process_group()
+"""
+
+
+@pytest.mark.parametrize("D", [2, 3])
+def test_p2p_two_processes_ipc(D):
+    """Two processes (one rank each) on the one GPU: hipIpcMemHandle exchange, verification
+    against the all-gather path, then 17 sweeps in two steps — bitwise equal to the unsharded run."""
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), CLV_ROOT=ROOT, CLV_D=str(D))
+        procs.append(subprocess.Popen([sys.executable, "-c", WORKER], env=env, cwd=ROOT, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    outs = []
+    for pr in procs:
+        try:
+            out, err = pr.communicate(timeout=240)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        outs.append((pr.returncode, out, err))
+    for rc, out, err in outs:
+        assert rc == 0, err[-3000:]
+        import json
+        res = json.loads(out.strip().splitlines()[-1])
+        assert res["ok"], res
