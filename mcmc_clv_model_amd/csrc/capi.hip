@@ -69,6 +69,10 @@ SweepArgs sweep_args(clv_sampler* s, int init, int fuse = 0) {
   a.mail = s->d_mail;
   a.peers = s->d_peers;
   a.rank = s->cfg.rank;
+  {  // CLV_PRE_VARIATES=0: draw the MH variates inside the MH phase (A/B measurements)
+    const char* env = std::getenv("CLV_PRE_VARIATES");
+    a.pre_variates = (env && std::string(env) == "0") ? 0 : 1;
+  }
   a.h = hyper_args(s, nullptr, 0);
   if (fuse) a.h.hvar = s->replay ? nullptr : s->d_hvar;
   return a;
@@ -323,7 +327,7 @@ int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* pri
   if (!s->replay && cfg->world_size == 1 && nb_local > 0 && bpu == 1 && nb_local <= 2 * BLOCK) {
     const char* env = std::getenv("CLV_PERSISTENT");
     hipDeviceProp_t prop{};
-    if (persist_occupancy(g.D, g.K, &s->persist_bpc) == hipSuccess &&
+    if (persist_occupancy(g.D, g.K, false, &s->persist_bpc) == hipSuccess &&
         hipGetDeviceProperties(&prop, s->device) == hipSuccess)
       s->n_cu = prop.multiProcessorCount;
     if ((!env || std::string(env) != "0") && (int64_t)s->persist_bpc * s->n_cu >= (int64_t)(nb_local + 1) * C)
@@ -335,7 +339,7 @@ int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* pri
   if (!s->replay && cfg->world_size > 1 && nb_local > 0 && nb_local <= 2 * BLOCK && g.n_units_global <= 2 * BLOCK &&
       bpu <= 64 && (int64_t)g.stride * ((nb_local + bpu - 1) / bpu) <= UMAIL) {
     hipDeviceProp_t prop{};
-    if (persist_occupancy(g.D, g.K, &s->persist_bpc) == hipSuccess &&
+    if (persist_occupancy(g.D, g.K, true, &s->persist_bpc) == hipSuccess &&
         hipGetDeviceProperties(&prop, s->device) == hipSuccess)
       s->n_cu = prop.multiProcessorCount;
     if ((int64_t)s->persist_bpc * s->n_cu >= (int64_t)(nb_local + 1) * C) {

@@ -105,6 +105,7 @@ struct SweepArgs {
   double* mail;              // this rank's mail buffer (device memory, polled by its level-2 workgroups)
   double* const* peers;      // [world] device pointers to every rank's mail buffer (peers[rank] = mail)
   int rank;
+  int pre_variates;          // persistent kernel: draw the next sweep's MH variates during the hand-off
   HyperArgs h;               // level-2 arguments of the fused tail
   unsigned long long* stamps; // diagnostic build only (CLV_STAMPS): [1024][8] s_memrealtime stamps
 };
@@ -122,7 +123,7 @@ hipError_t launch_sweep(const SweepArgs& a, bool replay, hipStream_t st, hipEven
 hipError_t launch_group(const GroupArgs& a, hipStream_t st);
 hipError_t launch_persist(const SweepArgs& a, int64_t s_first, int64_t n_sweeps, hipStream_t st,
                           hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
-hipError_t persist_occupancy(int D, int K, int* blocks_per_cu);
+hipError_t persist_occupancy(int D, int K, bool p2p, int* blocks_per_cu);
 hipError_t launch_hyper(const HyperArgs& a, bool replay, hipStream_t st);
 hipError_t launch_set_hyper(int D, int K, int n_chains, double* hyper, const double* beta_sigma,
                             double omega2, hipStream_t st);

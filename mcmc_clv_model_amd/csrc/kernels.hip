@@ -944,6 +944,48 @@ __device__ __forceinline__ void mh_run(Cust<D, K>& cu, const SlotPhilox& ph, dou
   for (int st = 0; st < MC; ++st) mh_step(cu, s00, s11, tl[st], tm[st], st < rem ? lu[st] : __builtin_inff(), exp_tab);
 }
 
+// Persistent kernel: the MH variates of a whole sweep (up to PRE_STEPS steps) drawn ahead, while
+// the wave would otherwise idle in the level-2 hand-off; the MH phase after (beta, Sigma) arrive is
+// then only the dependent fp64 accept/reject chain.  Steps >= S carry log U = +inf (never taken).
+constexpr int PRE_STEPS = 20;
+struct PreVariates {
+  float tl[PRE_STEPS], tm[PRE_STEPS], lu[PRE_STEPS];
+};
+
+__device__ __forceinline__ void mh_pre_variates(const SlotPhilox& ph, int S, PreVariates& v) {
+  constexpr int MC = MH_CHUNK_STEPS;
+#pragma unroll
+  for (int q = 0; q < PRE_STEPS / MC; ++q) {
+    float tl[MC], tm[MC], lu[MC];
+    if (q * MC < S) {  // wave-uniform
+      mh_chunk_variates(ph, (uint32_t)q, tl, tm, lu);
+    } else {
+#pragma unroll
+      for (int st = 0; st < MC; ++st) tl[st] = tm[st] = 0.0f;
+    }
+#pragma unroll
+    for (int st = 0; st < MC; ++st) {
+      v.tl[q * MC + st] = tl[st];
+      v.tm[q * MC + st] = tm[st];
+      v.lu[q * MC + st] = q * MC + st < S ? lu[st] : __builtin_inff();
+    }
+  }
+}
+
+template <int D, int K>
+__device__ __forceinline__ void mh_run_pre(Cust<D, K>& cu, const PreVariates& v, double s00, double s11, int S,
+                                           const double* exp_tab) {
+  constexpr int MC = MH_CHUNK_STEPS;
+#pragma unroll
+  for (int q = 0; q < PRE_STEPS / MC; ++q) {
+    if (q * MC < S) {  // wave-uniform
+#pragma unroll
+      for (int st = 0; st < MC; ++st)
+        mh_step(cu, s00, s11, v.tl[q * MC + st], v.tm[q * MC + st], v.lu[q * MC + st], exp_tab);
+    }
+  }
+}
+
 // Phase C1: state update (bi:337-338), draw_eta (tri:306-333), the likelihood term of stored
 // sweeps (bi:423-427) and the customer's sufficient statistics into acc.
 template <int D>
@@ -1323,7 +1365,7 @@ __device__ __forceinline__ bool wait_expired(uint64_t t0, Ctrl* ctrl, uint32_t p
 
 // The chain's level-2 workgroup of persist_kernel (one per chain, grid column nb_local).
 // register arrays (block/unit partials of the chain) do not raise the customer path's pressure.
-template <int D, int K>
+template <int D, int K, bool P2P>
 __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_first, int64_t n_sweeps, int c, uint32_t k0,
                                             uint32_t k1, int64_t wgi, int64_t it_stamp) {
   constexpr int NT = BLOCK;
@@ -1338,7 +1380,6 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
   __shared__ uint32_t s_abort;
   __shared__ double var_iw[4], var_chi[4], var_noise[32];
   __shared__ L2Scratch l2;
-  __shared__ double umail[UMAIL];  // world size > 1: this rank's unit partials [stat][local unit]
   const Geometry& g = a.g;
   const int tid = threadIdx.x;
   (void)wgi;
@@ -1397,7 +1438,7 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
     const int64_t per_rank = (int64_t)g.n_chains * NS * g.units_per_rank;  // mail doubles per rank and parity
     const double* mb = a.mail + (int64_t)(s & 1) * g.world_size * per_rank + (int64_t)c * NS * g.units_per_rank;
     const int64_t u0 = tid, u1 = tid + NT;  // global units this lane sums (n_units_global <= 2 NT)
-    if (g.world_size == 1) {
+    if constexpr (!P2P) {
 #pragma unroll
       for (int j = 0; j < NS; ++j) {
         acc[j] = 0.0;
@@ -1405,6 +1446,7 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
         if (b1 < g.nb_local) acc[j] += v1[j];
       }
     } else {
+      __shared__ double umail[UMAIL];  // this rank's unit partials [stat][local unit]
       // 3a. this rank's unit partials: blocks_per_unit consecutive blocks summed in group_kernel's
       //     order (a unit's blocks sit in consecutive lanes of one wavefront: bpu | 64)
       const int bpu = g.blocks_per_unit;
@@ -1528,7 +1570,9 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
   return;
 }
 
-template <int D, int K>
+// P2P: world size > 1 with the peer exchange (a separate instance, so that the world-size-1
+// kernel carries none of its registers or LDS).
+template <int D, int K, bool P2P>
 __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t s_first, int64_t n_sweeps) {
   constexpr int NT = BLOCK;
   constexpr int NXY = K * D;
@@ -1554,7 +1598,7 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
   if (tid == 0) s_abort = 0;
 
   if (b == g.nb_local) {  // the chain's level-2 workgroup
-    persist_level2<D, K>(a, s_first, n_sweeps, c, k0, k1, wgi, it_stamp);
+    persist_level2<D, K, P2P>(a, s_first, n_sweeps, c, k0, k1, wgi, it_stamp);
     return;
   }
 
@@ -1570,6 +1614,10 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
   if (tid < HS) Hs[tid] = a.hyper[(int64_t)c * HS + tid];  // sweep s_first: from before this launch
   __syncthreads();
   if (cu.active) cust_ztau<D, K, false>(cu, a, s_first, k0, k1, nullptr, exp_tab);
+  // MH variates drawn ahead (while the wave waits for the level-2 draw) when S fits the registers
+  const bool pre = a.pre_variates && g.S <= PRE_STEPS;
+  PreVariates pv;
+  if (cu.active && pre) mh_pre_variates(SlotPhilox(k0, k1, cu.gi, (uint32_t)s_first), g.S, pv);
   const double* hyp_c = a.hyp2 + (int64_t)c * HS;
   for (int64_t it = 0; it < n_sweeps; ++it) {
     const int64_t s = s_first + it;
@@ -1607,7 +1655,8 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
       CLV_P_STAMP(a.stamps, wgi, 2, stp);
       const double s00 = Hs[H_S00];
       const double s11 = Hs[H_S11];
-      mh_run(cu, SlotPhilox(k0, k1, cu.gi, (uint32_t)s), s00, s11, g.S, exp_tab);
+      if (pre) mh_run_pre(cu, pv, s00, s11, g.S, exp_tab);
+      else mh_run(cu, SlotPhilox(k0, k1, cu.gi, (uint32_t)s), s00, s11, g.S, exp_tab);
       CLV_P_STAMP(a.stamps, wgi, 3, stp);
       out = cust_finish<D, K, false, NS>(cu, a, s, stored, Hs, k0, k1, nullptr, exp_tab, acc);
     }
@@ -1619,7 +1668,10 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
     CLV_P_STAMP(a.stamps, wgi, 9, stp);
     if (cu.active) {
       cust_store<D, K>(cu, out, a, c, s, stored, false);
-      if (it + 1 < n_sweeps) cust_ztau<D, K, false>(cu, a, s + 1, k0, k1, nullptr, exp_tab);
+      if (it + 1 < n_sweeps) {
+        cust_ztau<D, K, false>(cu, a, s + 1, k0, k1, nullptr, exp_tab);
+        if (pre) mh_pre_variates(SlotPhilox(k0, k1, cu.gi, (uint32_t)(s + 1)), g.S, pv);
+      }
     }
     CLV_P_STAMP(a.stamps, wgi, 6, stp);
   }
@@ -1748,23 +1800,27 @@ hipError_t launch_persist(const SweepArgs& a, int64_t s_first, int64_t n_sweeps,
                           hipEvent_t e1) {
   const dim3 grid(a.g.nb_local + 1, a.g.n_chains);  // + the chain's level-2 workgroup
   const dim3 block(BLOCK);
-#define CLV_CASE(DD, KK, RR)                                                                                         \
-  if (a.g.D == DD && a.g.K == KK) {                                                                                \
-    if (e0) hipExtLaunchKernelGGL((persist_kernel<DD, KK>), grid, block, 0, st, e0, e1, 0, a, s_first, n_sweeps); \
-    else hipLaunchKernelGGL((persist_kernel<DD, KK>), grid, block, 0, st, a, s_first, n_sweeps);                  \
+#define CLV_CASE(DD, KK, PP)                                                                                         \
+  if (a.g.D == DD && a.g.K == KK && (a.g.world_size > 1) == PP) {                                                \
+    if (e0) hipExtLaunchKernelGGL((persist_kernel<DD, KK, PP>), grid, block, 0, st, e0, e1, 0, a, s_first, n_sweeps); \
+    else hipLaunchKernelGGL((persist_kernel<DD, KK, PP>), grid, block, 0, st, a, s_first, n_sweeps);                  \
     return hipGetLastError();                                                                                      \
   }
-  CLV_FOR_K(CLV_CASE, 2, 0)
-  CLV_FOR_K(CLV_CASE, 3, 0)
+  CLV_FOR_K(CLV_CASE, 2, false)
+  CLV_FOR_K(CLV_CASE, 3, false)
+  CLV_FOR_K(CLV_CASE, 2, true)
+  CLV_FOR_K(CLV_CASE, 3, true)
 #undef CLV_CASE
   return hipErrorInvalidValue;
 }
 
-hipError_t persist_occupancy(int D, int K, int* blocks_per_cu) {
-#define CLV_CASE(DD, KK, RR) \
-  if (D == DD && K == KK) return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, persist_kernel<DD, KK>, BLOCK, 0);
-  CLV_FOR_K(CLV_CASE, 2, 0)
-  CLV_FOR_K(CLV_CASE, 3, 0)
+hipError_t persist_occupancy(int D, int K, bool p2p, int* blocks_per_cu) {
+#define CLV_CASE(DD, KK, PP) \
+  if (D == DD && K == KK && p2p == PP) return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, persist_kernel<DD, KK, PP>, BLOCK, 0);
+  CLV_FOR_K(CLV_CASE, 2, false)
+  CLV_FOR_K(CLV_CASE, 3, false)
+  CLV_FOR_K(CLV_CASE, 2, true)
+  CLV_FOR_K(CLV_CASE, 3, true)
 #undef CLV_CASE
   return hipErrorInvalidValue;
 }
