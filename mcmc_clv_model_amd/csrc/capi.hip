@@ -68,6 +68,7 @@ SweepArgs sweep_args(clv_sampler* s, int init, int fuse = 0) {
   a.stamps = s->d_stamps;
   a.mail = s->d_mail;
   a.peers = s->d_peers;
+  a.wg_map = s->d_wgmap;
   a.rank = s->cfg.rank;
   {  // CLV_PRE_VARIATES=0: draw the MH variates inside the MH phase (A/B measurements)
     const char* env = std::getenv("CLV_PRE_VARIATES");
@@ -221,6 +222,73 @@ int64_t clv_replay_sweep_stride(const clv_sampler* s) {
   return n * (2 + 3 * (int64_t)s->g.S + (s->g.D == 3 ? 1 : 0)) + TAPE_HYPER;
 }
 
+namespace {
+// Persistent grid: which (chain, block) each dispatched workgroup runs.  The grid has more
+// workgroups (T = chains x (blocks + 1)) than CUs, and the dispatcher fills every CU once before
+// doubling up: linear workgroup i < T - n_cu shares its CU with workgroup i + n_cu (measured,
+// tools/placement.py).  A SIMD holding two customer waves runs each at ~0.68 of its solo speed,
+// and the hardware favours the older wave; pairing two waves of DIFFERENT chains lets the older
+// chain run ahead while the younger one crawls, and the run lasts until the slowest chain ends.
+// So shared CUs pair workgroups of the SAME chain (every chain then paces at its pairs' rate), each
+// chain's level-2 workgroup (asleep most of the time) shares a CU with one of its own customer
+// workgroups, and the pairs are spread evenly over the chains.  Pure placement: every workgroup
+// still runs one logical (chain, block), so results do not depend on it.
+std::vector<int32_t> persist_wg_map(int C, int nb, int n_cu) {
+  const int per = nb + 1;  // workgroups per chain (block nb = the level-2 workgroup)
+  const int T = C * per;
+  std::vector<int32_t> map(T);
+  for (int c = 0; c < C; ++c)  // identity: blockIdx = (b, c)
+    for (int b = 0; b < per; ++b) map[c * per + b] = (c << 16) | b;
+  const int P = T - n_cu;  // shared CUs
+  if (P <= 0 || T > 2 * n_cu) return map;
+  std::vector<std::vector<int>> todo(C);  // customer blocks of each chain still to place
+  for (int c = 0; c < C; ++c)
+    for (int b = nb - 1; b >= 0; --b) todo[c].push_back(b);
+  std::vector<int32_t> first, second, single;
+  int p = 0;
+  for (int c = 0; c < C && p < P; ++c, ++p) {  // level-2 workgroup + one own customer workgroup
+    first.push_back((c << 16) | nb);
+    if (todo[c].empty()) return map;
+    second.push_back((c << 16) | todo[c].back());
+    todo[c].pop_back();
+  }
+  const bool l2_paired = (int)first.size() == C;
+  for (int c = 0; p < P; c = (c + 1) % C) {  // same-chain customer pairs, round robin over chains
+    bool any = false;
+    for (int k = 0; k < C && !any; ++k) any = todo[(c + k) % C].size() >= 2;
+    if (!any) return map;  // cannot pair within chains: keep the identity
+    if (todo[c].size() < 2) continue;
+    first.push_back((c << 16) | todo[c].back());
+    todo[c].pop_back();
+    second.push_back((c << 16) | todo[c].back());
+    todo[c].pop_back();
+    ++p;
+  }
+  for (int c = 0; c < C; ++c) {
+    if (!l2_paired && c >= (int)first.size()) single.push_back((c << 16) | nb);
+    while (!todo[c].empty()) {
+      single.push_back((c << 16) | todo[c].back());
+      todo[c].pop_back();
+    }
+  }
+  // interleave the chains over the single slots (so that each chain spreads over all XCDs)
+  std::vector<int32_t> sorted_single;
+  for (size_t k = 0; sorted_single.size() < single.size(); ++k)
+    for (int c = 0; c < C; ++c) {
+      size_t seen = 0;
+      for (int32_t v : single)
+        if ((v >> 16) == c && seen++ == k) sorted_single.push_back(v);
+    }
+  if ((int)first.size() != P || (int)sorted_single.size() != n_cu - P) return map;
+  for (int i = 0; i < P; ++i) {
+    map[i] = first[i];
+    map[n_cu + i] = second[i];
+  }
+  for (int i = 0; i < n_cu - P; ++i) map[P + i] = sorted_single[i];
+  return map;
+}
+}  // namespace
+
 int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* prior, clv_sampler** out) {
   if (!cfg || !data || !prior || !out) return fail(CLV_EINVAL, "null argument");
   *out = nullptr;
@@ -350,6 +418,18 @@ int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* pri
       CLV_HIPC(dalloc(&s->d_peers, g.world_size));
     }
   }
+  if ((s->persistent || s->p2p_capable) && s->n_cu > 0) {
+    // default on for the bivariate model only: measured c2 13.44 -> 12.94 us per sweep, but c3
+    // (trivariate: longer level-2 draw, so both waves of a same-chain pair idle in the hand-off
+    // together) 16.36 -> 17.31.  CLV_WG_MAP=1 forces it, =0 disables it.
+    const char* env = std::getenv("CLV_WG_MAP");
+    const bool on = env ? std::string(env) != "0" : g.D == 2;
+    if (on) {
+      std::vector<int32_t> map = persist_wg_map((int)C, (int)nb_local, s->n_cu);
+      CLV_HIPC(dalloc(&s->d_wgmap, map.size()));
+      CLV_HIPC(hipMemcpy(s->d_wgmap, map.data(), sizeof(int32_t) * map.size(), hipMemcpyHostToDevice));
+    }
+  }
 #ifdef CLV_STAMPS
   {
     std::vector<unsigned long long> st(1024 * 8 + 12 * (size_t)C * (std::max(nb_local, 1) + 1), 0ull);
@@ -447,6 +527,7 @@ void clv_destroy(clv_sampler* s) {
   for (void* p : s->ipc_opened) (void)hipIpcCloseMemHandle(p);
   if (s->d_mail) (void)hipFree(s->d_mail);
   if (s->d_peers) (void)hipFree(s->d_peers);
+  if (s->d_wgmap) (void)hipFree(s->d_wgmap);
   if (s->own_stream && s->own) (void)hipStreamDestroy(s->own);
   delete s;
 }

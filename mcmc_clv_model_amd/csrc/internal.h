@@ -81,6 +81,7 @@ struct clv_sampler {
   bool p2p_ready = false;           // clv_p2p_connect done: clv_run runs persist_kernel
   double* d_mail = nullptr;         // [2][world][chain][stride][units_per_rank]
   double** d_peers = nullptr;       // [world] mail pointers (peers' opened IPC mappings, own d_mail)
+  int32_t* d_wgmap = nullptr;       // persistent grid: linear workgroup -> (chain << 16 | block)
   std::vector<void*> ipc_opened;    // hipIpcOpenMemHandle mappings to close
   double* d_hvar = nullptr;         // [chain][HV] precomputed hyper variates
   unsigned long long* d_stamps = nullptr;  // CLV_STAMPS diagnostic build only

@@ -105,6 +105,7 @@ struct SweepArgs {
   double* mail;              // this rank's mail buffer (device memory, polled by its level-2 workgroups)
   double* const* peers;      // [world] device pointers to every rank's mail buffer (peers[rank] = mail)
   int rank;
+  const int32_t* wg_map;     // persistent kernel: linear workgroup -> (chain << 16 | block), or null
   int pre_variates;          // persistent kernel: draw the next sweep's MH variates during the hand-off
   HyperArgs h;               // level-2 arguments of the fused tail
   unsigned long long* stamps; // diagnostic build only (CLV_STAMPS): [1024][8] s_memrealtime stamps

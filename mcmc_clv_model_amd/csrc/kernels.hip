@@ -1585,8 +1585,12 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
   __shared__ double Hs[HS];
   __shared__ uint32_t s_abort;
   const Geometry& g = a.g;
-  const int c = blockIdx.y;
-  const int b = blockIdx.x;
+  int c = blockIdx.y, b = blockIdx.x;
+  if (a.wg_map) {  // placement (capi.hip persist_wg_map): same-chain workgroups share CUs
+    const int32_t m = a.wg_map[blockIdx.y * gridDim.x + blockIdx.x];
+    c = m >> 16;
+    b = m & 0xFFFF;
+  }
   const int tid = threadIdx.x;
   const int64_t wgi = (int64_t)c * (g.nb_local + 1) + b;
   const int64_t it_stamp = n_sweeps >= 2 ? n_sweeps - 2 : 0;  // diagnostic build: one sweep's timeline
@@ -1666,6 +1670,9 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
     CLV_P_STAMP(a.stamps, wgi, 5, stp);
     CLV_P_STAMP(a.stamps, wgi, 8, stp);
     CLV_P_STAMP(a.stamps, wgi, 9, stp);
+#ifdef CLV_STAMPS
+    if (stp && a.stamps) a.stamps[1024 * 8 + wgi * 12 + 11] = blockIdx.y * gridDim.x + blockIdx.x;  // dispatch position
+#endif
     if (cu.active) {
       cust_store<D, K>(cu, out, a, c, s, stored, false);
       if (it + 1 < n_sweeps) {
