@@ -162,10 +162,27 @@ def cpu_baseline(workload: str, warm: int = 20, timed: int = 200):
                          capture_output=True, text=True, env=env, check=True, timeout=900)
     r = json.loads(out.stdout.strip().splitlines()[-1])
     n = len(load_workload(workload)[0])
-    return dict(value=r["value"], unit="customer-sweeps/s", cores=1, kind="port",
-                s_per_sweep=r["s_per_sweep"],
-                sample=f"oracle/ref_cpu.py (numpy restatement, bitwise equal to the reference) on {workload}: "
-                       f"1 chain x {n} customers, {timed} timed sweeps after {warm} warm-up sweeps, 1 thread")
+    res = dict(value=r["value"], unit="customer-sweeps/s", cores=1, kind="port",
+               s_per_sweep=r["s_per_sweep"],
+               sample=f"oracle/ref_cpu.py (numpy restatement, bitwise equal to the reference) on {workload}: "
+                      f"1 chain x {n} customers, {timed} timed sweeps after {warm} warm-up sweeps, 1 thread")
+    # also an all-cores throughput — P independent single-threaded chains in P
+    # processes at once (the reference runs its chains sequentially; this is its best case)
+    procs = min(16, os.cpu_count() or 1)  # the GPU box's CPU share is 16 (gpurun)
+    t_warm, t_timed = max(2, warm // 4), max(5, timed // 4)
+    ps = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--cpu-baseline-child", "--workload", workload,
+                            "--cpu-warm", str(t_warm), "--cpu-timed", str(t_timed)],
+                           stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True, env=env) for _ in range(procs)]
+    vals = []
+    for p in ps:
+        o, _ = p.communicate(timeout=900)
+        if p.returncode == 0:
+            vals.append(json.loads(o.strip().splitlines()[-1])["value"])
+    if len(vals) == procs:
+        res["all_cores"] = dict(value=sum(vals), cores=procs,
+                                sample=f"{procs} processes x 1 chain, {t_timed} timed sweeps each after {t_warm}, "
+                                       "1 thread each, run concurrently")
+    return res
 
 
 def main():
