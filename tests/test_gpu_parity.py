@@ -402,19 +402,23 @@ def _run_mode(p, persistent, sweeps, chunks, **kw):
     return info, st, l1, l2, ll, sums
 
 
-@pytest.mark.parametrize("D,covs,n,sink", [(2, ["first_sales_scaled"], 23570, "full"),
-                                           (3, ["gender_F", "age_scaled"], 23570, "summary"),
-                                           (2, [], 1000, "full"), (3, ["gender_F"], 300, "full")])
-def test_persistent_kernel_bitwise_equals_launch_per_sweep(L, D, covs, n, sink):
+@pytest.mark.parametrize("D,covs,n,sink,S", [(2, ["first_sales_scaled"], 23570, "full", 20),
+                                             (3, ["gender_F", "age_scaled"], 23570, "summary", 20),
+                                             (2, [], 1000, "full", 20), (3, ["gender_F"], 300, "full", 20),
+                                             (2, ["first_sales_scaled"], 2357, "full", 7),
+                                             (3, ["gender_F"], 2357, "summary", 23)])
+def test_persistent_kernel_bitwise_equals_launch_per_sweep(L, D, covs, n, sink, S):
     """World size 1: the persistent kernel (one launch for all of a clv_run's sweeps, sentinel-slot
     hand-off to a level-2 workgroup per chain) is chosen by default where the grid fits at once,
     and reproduces the launch-per-sweep path (fused level-2 tail) bit for bit — state, draws,
     level-2 records, log-likelihood, summaries — across clv_run calls of uneven length (the
-    carried state at each launch boundary), burn-in and thinning."""
+    carried state at each launch boundary), burn-in and thinning; S = 7 (a partial last chunk of
+    drawn-ahead variates) and S = 23 (more steps than the drawn-ahead registers hold: variates
+    drawn within the sweep)."""
     df = cdnow("full", n) if n > 2357 else cdnow("abe", n)
     from mcmc_clv_model_amd.sampler import build_problem
     p = build_problem(df, covs, D)
-    kw = dict(mcmc=25, burnin=6, thin=3, chains=3, seed=2024, draw_sink=sink)
+    kw = dict(mcmc=25, burnin=6, thin=3, chains=3, seed=2024, draw_sink=sink, n_mh_steps=S)
     chunks = (1, 7, 2, 20, 1)
     a = _run_mode(p, True, 31, chunks, **kw)
     b = _run_mode(p, False, 31, chunks, **kw)
