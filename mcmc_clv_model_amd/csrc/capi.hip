@@ -404,7 +404,7 @@ int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* pri
   // World size > 1: the same persistent kernel exchanging unit partials with its peers over xGMI
   // (clv_p2p_connect) when the grid fits at once here, as above, and on every rank (the caller
   // checks that all ranks are capable before connecting).
-  if (!s->replay && cfg->world_size > 1 && nb_local > 0 && nb_local <= 2 * BLOCK && g.n_units_global <= 2 * BLOCK &&
+  if (!s->replay && cfg->world_size > 1 && cfg->world_size <= MAX_WORLD && nb_local > 0 && nb_local <= 2 * BLOCK && g.n_units_global <= 2 * BLOCK &&
       bpu <= 64 && (int64_t)g.stride * ((nb_local + bpu - 1) / bpu) <= UMAIL) {
     hipDeviceProp_t prop{};
     if (persist_occupancy(g.D, g.K, true, &s->persist_bpc) == hipSuccess &&

@@ -10,6 +10,7 @@ namespace clv {
 constexpr int BLOCK = CLV_BLOCK;       // customers (lanes) per sweep workgroup
 constexpr int HS = 64;                 // doubles of hyper state per chain
 constexpr int TAPE_HYPER = 40;         // doubles of hyper variates per recorded sweep
+constexpr int MAX_WORLD = 64;             // peer exchange: ranks (mail pointers staged in LDS)
 constexpr int UMAIL = 2048;            // persistent kernel, world size > 1: LDS doubles for this rank's
                                        // unit partials (stride * local units must fit)
 constexpr int HV = 40;                 // precomputed Philox hyper variates per chain: iw normals [0,3),

@@ -92,7 +92,17 @@ __device__ __forceinline__ double add_row_ror(double x) {
 // ceil(NS/4) values — ~3 VALU per element-step, instead of 6 ds_bpermute butterflies of all NS
 // values.  Lane 0 of each row writes its row's values; waves are summed in fixed order.
 // Result valid in `out` (LDS) for all threads after the call.
-template <int NS, int NT = BLOCK>
+// Workgroup barrier ordering LDS accesses only: unlike __syncthreads it does not wait for the
+// wave's outstanding global loads/stores (vmcnt), so write-through or remote stores issued before
+// it stay in flight.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// LDS_ONLY: its barriers are lds_barrier() (callers with stores in flight that need no ordering).
+template <int NS, int NT = BLOCK, bool LDS_ONLY = false>
 __device__ __forceinline__ void block_reduce(double (&v)[NS], double (*red)[NS], double* out) {
   constexpr int H1 = (NS + 1) / 2;
   constexpr int H2 = (H1 + 1) / 2;
@@ -133,14 +143,14 @@ __device__ __forceinline__ void block_reduce(double (&v)[NS], double (*red)[NS],
       if (i1 < H1 && idx < NS) red[wave][idx] = w2[j];
     }
   }
-  __syncthreads();
+  if constexpr (LDS_ONLY) lds_barrier(); else __syncthreads();
   if (threadIdx.x < NS) {
     double t = red[0][threadIdx.x];
 #pragma unroll
     for (int w = 1; w < NW; ++w) t += red[w][threadIdx.x];
     out[threadIdx.x] = t;
   }
-  __syncthreads();
+  if constexpr (LDS_ONLY) lds_barrier(); else __syncthreads();
 }
 
 // bi:402 (the reference's loop ends at burnin + mcmc, bi:383, so nothing beyond is stored)
@@ -1380,11 +1390,15 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
   __shared__ uint32_t s_abort;
   __shared__ double var_iw[4], var_chi[4], var_noise[32];
   __shared__ L2Scratch l2;
+  __shared__ double* s_peers[P2P ? MAX_WORLD : 1];  // every rank's mail (loaded once)
   const Geometry& g = a.g;
   const int tid = threadIdx.x;
   (void)wgi;
   double* parts = a.blockpart + (int64_t)c * g.stride * g.blocks_per_rank;  // [stat][block]
   if (tid == 0) s_abort = 0;
+  if constexpr (P2P) {
+    if (tid < g.world_size) s_peers[tid] = a.peers[tid];
+  }
   __syncthreads();
   // ================= the chain's level-2 workgroup =================
   // It shares its CU with customer workgroups; it is on every sweep's critical path, so its
@@ -1407,7 +1421,22 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
     // 2. wait for every block partial of sweep s (lane tid: blocks tid, tid + NT, ...; nb <= 2 NT)
     double v0[NS], v1[NS];
     const int b0 = tid, b1 = tid + NT;
-    {  // each wavefront polls on its own (no barrier per poll); a lane stops once its slots are full
+    // P2P: the global units this lane sums (u0, u1: as hyper_body, n_units_global <= 2 NT) and
+    // where they come from — another rank's (the mail) or this rank's own (LDS, formed below)
+    const int64_t per_rank = (int64_t)g.n_chains * NS * g.units_per_rank;  // mail doubles per rank and parity
+    const double* mb = a.mail + (int64_t)(s & 1) * g.world_size * per_rank + (int64_t)c * NS * g.units_per_rank;
+    const int64_t u0 = tid, u1 = tid + NT;
+    const int r0 = (int)(u0 / g.units_per_rank), r1 = (int)(u1 / g.units_per_rank);
+    const int l0 = (int)(u0 % g.units_per_rank), l1 = (int)(u1 % g.units_per_rank);
+    const double* p0 = mb + r0 * per_rank + l0;
+    const double* p1 = mb + r1 * per_rank + l1;
+    const bool h0 = u0 < g.n_units_global, h1 = u1 < g.n_units_global;
+    const bool m0 = P2P && h0 && r0 != a.rank, m1 = P2P && h1 && r1 != a.rank;
+    double w0[NS], w1[NS];
+    bool mdone = !(m0 || m1);  // this lane's mail slots all full (or none to read)
+    {  // each wavefront polls on its own (no barrier per poll); a lane stops once its slots are full.
+       // P2P: the mail is polled alongside (the other ranks' units of the last rank to finish are
+       // then already in registers when its own partials are complete)
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       bool done = false;
       for (uint32_t poll = 0;; ++poll) {
@@ -1422,6 +1451,19 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
           for (int j = 0; j < NS; ++j) ok = ok && slot_full(v0[j]) && slot_full(v1[j]);
           done = ok;
         }
+        if constexpr (P2P) {
+          if (!mdone) {
+            bool ok = true;
+#pragma unroll
+            for (int j = 0; j < NS; ++j) {
+              w0[j] = m0 ? ld_sys(p0 + (int64_t)j * g.units_per_rank) : 0.0;
+              w1[j] = m1 ? ld_sys(p1 + (int64_t)j * g.units_per_rank) : 0.0;
+            }
+#pragma unroll
+            for (int j = 0; j < NS; ++j) ok = ok && slot_full(w0[j]) && slot_full(w1[j]);
+            mdone = ok;
+          }
+        }
         if (__all(done)) break;
         if (wait_expired(t0, a.ctrl_rw, poll)) {
           s_abort = 1;
@@ -1435,9 +1477,6 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
     CLV_P_STAMP(a.stamps, wgi, 2, stp);
     // 3. the fused path's fixed-order sum (hyper_body: lane u sums units u, u + NT, ... in order)
     double acc[NS];
-    const int64_t per_rank = (int64_t)g.n_chains * NS * g.units_per_rank;  // mail doubles per rank and parity
-    const double* mb = a.mail + (int64_t)(s & 1) * g.world_size * per_rank + (int64_t)c * NS * g.units_per_rank;
-    const int64_t u0 = tid, u1 = tid + NT;  // global units this lane sums (n_units_global <= 2 NT)
     if constexpr (!P2P) {
 #pragma unroll
       for (int j = 0; j < NS; ++j) {
@@ -1448,72 +1487,85 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
     } else {
       __shared__ double umail[UMAIL];  // this rank's unit partials [stat][local unit]
       // 3a. this rank's unit partials: blocks_per_unit consecutive blocks summed in group_kernel's
-      //     order (a unit's blocks sit in consecutive lanes of one wavefront: bpu | 64)
+      //     order (a unit's blocks sit in consecutive lanes of one wavefront: bpu | 64); with one
+      //     block per unit the unit partial IS the block partial (the sharded path has no group
+      //     kernel then)
       const int bpu = g.blocks_per_unit;
       const int ul = (g.nb_local + bpu - 1) / bpu;
       const int lane = tid & 63;
+      double t0[NS], t1[NS];
+      if (bpu == 1) {
 #pragma unroll
-      for (int j = 0; j < NS; ++j) {
-        double t0 = 0.0, t1 = 0.0;
-        for (int k = 0; k < bpu; ++k) {
-          t0 += __shfl(v0[j], lane + k, 64);  // blocks >= nb_local contribute 0.0, as group_kernel's
-          t1 += __shfl(v1[j], lane + k, 64);  // zero-initialised padding blocks do
+        for (int j = 0; j < NS; ++j) {
+          t0[j] = v0[j];
+          t1[j] = v1[j];
         }
-        if (tid % bpu == 0) {
-          if (tid / bpu < ul) umail[j * ul + tid / bpu] = t0;
-          if ((tid + NT) / bpu < ul) umail[j * ul + (tid + NT) / bpu] = t1;
+      } else {
+#pragma unroll
+        for (int j = 0; j < NS; ++j) {
+          t0[j] = 0.0 + v0[j];
+          t1[j] = 0.0 + v1[j];
+        }
+        for (int k = 1; k < bpu; ++k) {  // all statistics' shuffles of one k in flight together
+#pragma unroll
+          for (int j = 0; j < NS; ++j) {
+            t0[j] += __shfl(v0[j], lane + k, 64);  // blocks >= nb_local contribute 0.0, as
+            t1[j] += __shfl(v1[j], lane + k, 64);  // group_kernel's zero-initialised padding does
+          }
         }
       }
-      __syncthreads();
-      // 3b. to every rank's mail slot of sweep s (write-through stores over xGMI; the value is
-      //     its own arrival flag — the sentinel never occurs in a partial)
+      if (tid % bpu == 0) {
+#pragma unroll
+        for (int j = 0; j < NS; ++j) {
+          if (tid / bpu < ul) umail[j * ul + tid / bpu] = t0[j];
+          if ((tid + NT) / bpu < ul) umail[j * ul + (tid + NT) / bpu] = t1[j];
+        }
+      }
+      lds_barrier();
+      CLV_P_STAMP(a.stamps, wgi, 10, stp);
+      // 3b. to every OTHER rank's mail slot of sweep s (write-through stores over xGMI; the value
+      //     is its own arrival flag — the sentinel never occurs in a partial); own units stay in LDS
       const int64_t dst = ((int64_t)(s & 1) * g.world_size + a.rank) * per_rank + (int64_t)c * NS * g.units_per_rank;
       for (int e = tid; e < NS * ul; e += NT) {
         const int j = e / ul, lu = e - j * ul;
         const double v = umail[e];
-        for (int q = 0; q < g.world_size; ++q) st_sys(a.peers[q] + dst + (int64_t)j * g.units_per_rank + lu, v);
+        for (int q = 0; q < g.world_size; ++q)
+          if (q != a.rank) st_sys(s_peers[q] + dst + (int64_t)j * g.units_per_rank + lu, v);
       }
-      // 3c. wait for every rank's units in this rank's mail, then the fixed-order sum
-      double w0[NS], w1[NS];
-      const double* p0 = mb + (u0 / g.units_per_rank) * per_rank + (u0 % g.units_per_rank);
-      const double* p1 = mb + (u1 / g.units_per_rank) * per_rank + (u1 % g.units_per_rank);
-      const bool h0 = u0 < g.n_units_global, h1 = u1 < g.n_units_global;
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      bool done = false;
-      for (uint32_t poll = 0;; ++poll) {
-        if (!done) {
+      // 3c. the other ranks' units not seen yet
+      const uint64_t tw = __builtin_amdgcn_s_memrealtime();
+      for (uint32_t poll = 0; !__all(mdone); ++poll) {
+        if (!mdone) {
           bool ok = true;
 #pragma unroll
           for (int j = 0; j < NS; ++j) {
-            w0[j] = h0 ? ld_sys(p0 + (int64_t)j * g.units_per_rank) : 0.0;
-            w1[j] = h1 ? ld_sys(p1 + (int64_t)j * g.units_per_rank) : 0.0;
+            w0[j] = m0 ? ld_sys(p0 + (int64_t)j * g.units_per_rank) : 0.0;
+            w1[j] = m1 ? ld_sys(p1 + (int64_t)j * g.units_per_rank) : 0.0;
           }
 #pragma unroll
           for (int j = 0; j < NS; ++j) ok = ok && slot_full(w0[j]) && slot_full(w1[j]);
-          done = ok;
+          mdone = ok;
         }
-        if (__all(done)) break;
-        if (wait_expired(t0, a.ctrl_rw, poll)) {
+        if (__all(mdone)) break;
+        if (wait_expired(tw, a.ctrl_rw, poll)) {
           s_abort = 1;
           break;
         }
         __builtin_amdgcn_s_sleep(1);
       }
-      __syncthreads();
+      CLV_P_STAMP(a.stamps, wgi, 11, stp);
+      lds_barrier();  // (the stores to the peers stay in flight)
       if (s_abort) return;
 #pragma unroll
       for (int j = 0; j < NS; ++j) {
+        const double x0 = m0 ? w0[j] : (h0 ? umail[j * ul + l0] : 0.0);
+        const double x1 = m1 ? w1[j] : (h1 ? umail[j * ul + l1] : 0.0);
         acc[j] = 0.0;
-        if (h0) acc[j] += w0[j];
-        if (h1) acc[j] += w1[j];
-      }
-#pragma unroll
-      for (int j = 0; j < NS; ++j) {  // empty again before any rank can write sweep s + 2 here
-        if (h0) st_sys((double*)p0 + (int64_t)j * g.units_per_rank, slot_empty());
-        if (h1) st_sys((double*)p1 + (int64_t)j * g.units_per_rank, slot_empty());
+        if (h0) acc[j] += x0;
+        if (h1) acc[j] += x1;
       }
     }
-    block_reduce<NS, NT>(acc, red, tot);  // also publishes the variates (LDS)
+    block_reduce<NS, NT, P2P>(acc, red, tot);  // also publishes the variates (LDS)
     CLV_P_STAMP(a.stamps, wgi, 6, stp);
     // 4. reset: the partial slots (their writers write again only after step 6) and the
     //    (beta, Sigma) set every reader of s has read (its next write is for s+2)
@@ -1523,6 +1575,15 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
       if (b1 < g.nb_local) st_wt(parts + (int64_t)j * g.blocks_per_rank + b1, slot_empty());
     }
     if (it > 0 && tid < HS) st_wt(a.hyp2 + ((int64_t)(s & 1) * g.n_chains + c) * HS + tid, slot_empty());
+    if constexpr (P2P) {  // this rank's mail slots of sweep s: empty again before any rank can
+                          // write sweep s + 2 there (only after this rank's units of s + 1, which
+                          // leave after the vmcnt(0) below)
+#pragma unroll
+      for (int j = 0; j < NS; ++j) {
+        if (m0) st_sys((double*)p0 + (int64_t)j * g.units_per_rank, slot_empty());
+        if (m1) st_sys((double*)p1 + (int64_t)j * g.units_per_rank, slot_empty());
+      }
+    }
     if (tid < HS) Hs[tid] = 0.0;  // unwritten hyper slots publish as 0 (wavefront 0: ordered before the draw's writes)
     // 5. the draw (wavefront 0) while the resets drain
     level2_draw<D, K>(tot, var_iw, var_chi, var_noise, false, &l2, l2.Ai);
