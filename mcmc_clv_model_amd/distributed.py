@@ -169,6 +169,13 @@ class ShardedSampler:
         the peer path only if every rank's state is bitwise identical (else RCCL, or an error
         when ``required``)."""
         import torch.distributed as dist
+        if verify_sweeps > 0 and self.s.sweeps_done + verify_sweeps > self.s.burnin:
+            # the check replays sweeps from a saved state: only burn-in sweeps (nothing stored twice)
+            if required:
+                raise ValueError("verify_sweeps must fit in the burn-in (nothing may be stored twice); "
+                                 "pass verify_sweeps=0 to skip the check")
+            self.p2p_note = "not verified (burn-in shorter than verify_sweeps): all-gather path kept"
+            return
         capable = self._all_ok(self.s.p2p_info()["capable"])
         if not capable:
             if required:
@@ -190,8 +197,6 @@ class ShardedSampler:
         dist.barrier(group=self.group)
         if verify_sweeps > 0:
             n0 = self.s.sweeps_done
-            if n0 + verify_sweeps > self.s.burnin:
-                raise ValueError("verify_sweeps must fit in the burn-in (nothing may be stored twice)")
             snap = self.s.get_state()
             self._eager(verify_sweeps)
             self.synchronize()
