@@ -209,6 +209,9 @@ int clv_debug_hyper_variates(uint64_t seed, int32_t chain, uint32_t sweep, doubl
                              double* chi2, double* normals);
 /* The Philox-mode MH step's fp64 exp (csrc/fastmath.h, |x| <= 700) on n values. */
 int clv_debug_exp(const double* x, int64_t n, double* out);
+/* Host only (no device): the persistent grid's placement map for n_chains chains of nb customer
+ * workgroups (+1 level-2 workgroup each) on n_cu CUs — out[linear workgroup] = chain << 16 | block. */
+int clv_debug_wg_map(int32_t n_chains, int32_t nb, int32_t n_cu, int32_t* out);
 
 /* ---- Posterior analysis on device ----
  * Inputs are level-1 draws [n_draws][n][width] in the reference's layout, chains stacked

@@ -112,6 +112,7 @@ def lib() -> ctypes.CDLL:
         "clv_debug_stamps": (c_int32, [sp, POINTER(c_uint64)]),
         "clv_debug_wg_stamps": (c_int32, [sp, POINTER(c_uint64)]),
         "clv_debug_exp": (c_int32, [dp, c_int64, dp]),
+        "clv_debug_wg_map": (c_int32, [c_int32, c_int32, c_int32, POINTER(c_int32)]),
         "clv_predict": (c_int32, [c_int32, dp, c_int64, c_int64, c_int32, dp, c_double, c_uint64, c_int32, c_double,
                                   POINTER(c_int64), dp]),
         "clv_predict_sampler": (c_int32, [sp, c_double, c_uint64, c_int32, c_double, POINTER(c_int64), dp]),

@@ -984,6 +984,14 @@ int clv_debug_hyper_variates(uint64_t seed, int32_t chain, uint32_t sweep, doubl
   return CLV_OK;
 }
 
+int clv_debug_wg_map(int32_t n_chains, int32_t nb, int32_t n_cu, int32_t* out) {
+  if (!out || n_chains < 1 || nb < 0 || n_cu < 1 || n_chains >= (1 << 15) || nb >= (1 << 16))
+    return fail(CLV_EINVAL, "bad arguments");
+  const std::vector<int32_t> m = persist_wg_map(n_chains, nb, n_cu);
+  std::copy(m.begin(), m.end(), out);
+  return CLV_OK;
+}
+
 int clv_debug_exp(const double* x, int64_t n, double* out) {
   if (!x || !out || n < 1) return fail(CLV_EINVAL, "bad arguments");
   double *dx, *dout;

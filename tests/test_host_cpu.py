@@ -238,3 +238,31 @@ def test_philox_header_host_build_kat_and_hoisting(tmp_path):
     out = subprocess.run([exe], capture_output=True, text=True)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "mismatches 0" in out.stdout
+
+
+@pytest.mark.parametrize("C,nb,n_cu", [(4, 93, 256), (3, 93, 256), (4, 94, 256), (2, 200, 256), (8, 40, 256),
+                                       (1, 300, 256), (4, 40, 256), (4, 200, 256)])
+def test_persistent_placement_map(C, nb, n_cu):
+    """clv_debug_wg_map (host code, capi.hip persist_wg_map): the placement of the persistent grid is
+    a permutation of every (chain, block) incl. each chain's level-2 workgroup; when the grid has
+    more workgroups than CUs (but at most two per CU), the workgroups dispatched onto the same CU
+    (linear i and i + n_cu) belong to the same chain, and each level-2 workgroup shares its CU with
+    one of its own chain's customer workgroups; otherwise the identity."""
+    from mcmc_clv_model_amd import _lib
+    L = _lib.lib()
+    T = C * (nb + 1)
+    out = (ctypes.c_int32 * T)()
+    assert L.clv_debug_wg_map(C, nb, n_cu, out) == 0
+    m = np.array(out[:], dtype=np.int64)
+    chain, block = m >> 16, m & 0xFFFF
+    assert sorted(zip(chain.tolist(), block.tolist())) == [(c, b) for c in range(C) for b in range(nb + 1)]
+    P = T - n_cu
+    if P <= 0 or T > 2 * n_cu:
+        assert np.array_equal(m, [(c << 16) | b for c in range(C) for b in range(nb + 1)])
+        return
+    for i in range(P):
+        assert chain[i] == chain[i + n_cu], (i, chain[i], chain[i + n_cu])
+    l2 = np.flatnonzero(block == nb)
+    assert all(i < P or i >= n_cu for i in l2)  # every level-2 workgroup sits on a shared CU
+    pairs = np.bincount(chain[:P], minlength=C)
+    assert pairs.max() - pairs.min() <= 1  # shared CUs spread evenly over the chains
