@@ -13,10 +13,10 @@ mail over xGMI (after a bitwise check against the RCCL path), else one RCCL all_
 Prints ONE JSON line (rank 0).  value = chains * customers * steps / wall time of the timed
 region (world size 1: one persistent-kernel launch when the grid fits at once, else hipGraph
 replay of the fused sweep launches; max over ranks).  roofline: the dominant kernel's algorithmic
-bytes per launch / its launch duration, measured with HIP start/stop
-events on the launch(es) of a second timed pass over further sweeps of the same run (per-launch
-events force host-issued launches, so that pass gives kernel durations, not `value`); traffic
-from the committed rocprofv3 PMC summary.  cpu_baseline: the bitwise-pinned numpy restatement of
+bytes per launch / its launch duration, measured with HIP start/stop events — for the persistent
+kernel on the timed region's own launch; for launch-per-sweep paths on the launches of a second
+pass over further sweeps of the same run (per-launch events force host-issued launches, so that
+pass gives kernel durations, not `value`); traffic from the committed rocprofv3 PMC summary.  cpu_baseline: the bitwise-pinned numpy restatement of
 the reference (oracle/ref_cpu.py) on 1 core.
 """
 from __future__ import annotations
@@ -262,14 +262,23 @@ def main():
     sync()
     if dist:
         dist.barrier()
+    # persistent kernel: the timed launch itself carries the HIP start/stop events (the dispatch's
+    # own timestamps via hipExtLaunchKernelGGL on the sampler's stream — no extra packets)
+    live = timing and persistent
+    if live:
+        kern.set_timing(True)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    run(a.steps)                      # timed region: hipGraph replay (world 1) / sharded steps
+    run(a.steps)                      # timed region: persistent launch / hipGraph replay / sharded steps
     sync()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     dt = time.perf_counter() - t0
+    kt_live = None
+    if live:
+        kt_live = kern.kernel_time()
+        kern.set_timing(False)
     if dist:
         t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local_rank}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -277,20 +286,28 @@ def main():
     units = chains * n_total * a.steps
     value = units / dt
 
-    # Roofline pass: the same sweeps continue, each sweep launch carrying HIP start/stop events
-    # (hipExtLaunchKernelGGL: the dispatch's own timestamps).  Launches are then host-issued,
-    # which leaves gaps between kernels, so this pass yields kernel durations, not `value`.
+    # Launch-per-sweep paths: a roofline pass continues the same sweeps with HIP start/stop events
+    # on every sweep launch (hipExtLaunchKernelGGL: the dispatch's own timestamps).  Launches are
+    # then host-issued, which leaves gaps between kernels, so that pass yields kernel durations,
+    # not `value`.  The persistent kernel's durations come from the timed launch itself.
     roofline = None
     n_local = kern.n
-    frac = stored_fraction(burnin, thin, a.warmup + a.steps + 1, a.warmup + a.steps + min(a.steps, a.timing_steps))
+    if live:
+        n_t = a.steps
+        frac = stored_fraction(burnin, thin, a.warmup + 1, a.warmup + a.steps)
+    else:
+        n_t = min(a.steps, a.timing_steps)
+        frac = stored_fraction(burnin, thin, a.warmup + a.steps + 1, a.warmup + a.steps + n_t)
     bpu = algorithmic_bytes(D, K, frac, sink)
     if timing:
-        kern.set_timing(True)
-        n_t = min(a.steps, a.timing_steps)
-        run(n_t)
-        sync()
-        kt = kern.kernel_time()
-        kern.set_timing(False)
+        if live:
+            kt = kt_live
+        else:
+            kern.set_timing(True)
+            run(n_t)
+            sync()
+            kt = kern.kernel_time()
+            kern.set_timing(False)
         if kt["sweep_launches"]:
             # kt["sweep_launches"] counts sweeps; the persistent kernel runs all n_t in ONE launch
             t_sweep = kt["sweep_ms"] / kt["sweep_launches"] * 1e-3
@@ -307,7 +324,9 @@ def main():
                             ("sweep_kernel (incl. fused level-2 tail)" if not sharded else "sweep_kernel"),
                             bytes_per_unit=round(bpu, 3), units_per_launch=units, sweeps_per_launch=spl,
                             launch_us=round(t_launch * 1e6, 3), sweep_kernel_us=round(t_sweep * 1e6, 3),
-                            timed_launches=kt["sweep_launches"] // spl)
+                            timed_launches=kt["sweep_launches"] // spl,
+                            events=("the timed region's launch" if live else
+                                    f"a roofline pass of {n_t} further sweeps, one event pair per launch"))
             tr = committed_traffic(a.workload, sharded and not p2p, kname)
             if tr:  # HBM bytes per launch (calibrated PMC), per sweep x sweeps per launch
                 roofline["traffic"] = round(tr["bytes_per_sweep"] * spl)
