@@ -39,11 +39,17 @@ def _run_envelope(name, M=16, seed=777):
 
 @pytest.mark.parametrize("name", ["c1_bi_k1", "abe_bi_k2", "abe_tri_k3"])
 def test_posterior_envelope_vs_reference_ensemble(name):
-    """Per customer: |mean_gpu - mean_ref| <= 4 * sqrt(sd_ref^2/M + sd_gpu^2/M) for >= 99% of
-    customers; population means within 4 standard errors; per level-2 parameter, the mean of the
-    chains' posterior medians differs by <= 4.5 two-sample standard errors (M = 16 vs 16 chains).
-    Calibration: two independent 8-chain ensembles of the reference itself differ by up to
-    |z| = 2.8 on Sigma01/Sigma11, which mix slowly at 2000 + 2000 sweeps."""
+    """Population means within 4 standard errors of the chain-to-chain spread (the common shift of
+    every customer that the slowly mixing hyper-parameters cause); per customer, after that common
+    shift is removed, |z| <= 4 with z = (mean_gpu - mean_ref) / sqrt(sd_ref^2/M + sd_gpu^2/M) for
+    >= 99% of customers; per level-2 parameter, the mean of the chains' posterior medians differs by
+    <= 4.5 two-sample standard errors (M = 16 vs 16 chains).
+    Calibration (tools/envelope_ref_calibration.py, tools/envelope_seeds.py): three further 16-chain
+    ensembles of the reference itself score, on c1 (M1, 2000 + 2000 sweeps), mean per-customer z
+    -0.7 / -2.0 / -1.4 against the fixture's ensemble and population z down to -3.5 — so the
+    UNcentred per-customer fraction fails for the reference itself (0.958, 0.988) while the centred
+    one stays >= 0.991; five GPU ensembles score centred >= 0.997, population |z| <= 2.7.  Two
+    independent 8-chain reference ensembles also differ by up to |z| = 2.8 on Sigma01/Sigma11."""
     f, g, d = _run_envelope(name)
     M_ref = int(f["M"])
     for k, v in g.items():
@@ -52,8 +58,8 @@ def test_posterior_envelope_vs_reference_ensemble(name):
         m_r, s_r = f[k + "_mean"], f[k + "_sd"]
         se = np.sqrt(np.maximum(s_r, SD_FLOOR[k]) ** 2 / M_ref + np.maximum(s_g, SD_FLOOR[k]) ** 2 / M)
         z = (m_g - m_r) / se
-        frac = np.mean(np.abs(z) <= 4.0)
-        assert frac >= 0.99, f"{name}/{k}: only {frac:.4f} of customers within 4 sigma"
+        frac = np.mean(np.abs(z - z.mean()) <= 4.0)  # the common shift is the population test below
+        assert frac >= 0.99, f"{name}/{k}: only {frac:.4f} of customers within 4 sigma (mean z {z.mean():+.2f})"
         pop_r = f[k + "_chains"]
         pop_g = v.mean(1)
         se_pop = np.sqrt(pop_r.var(ddof=1) / M_ref + pop_g.var(ddof=1) / M)

@@ -18,5 +18,8 @@ for name in sys.argv[1].split(","):
             m_r, s_r = f[k + "_mean"], f[k + "_sd"]
             se = np.sqrt(np.maximum(s_r, SD_FLOOR[k]) ** 2 / M_ref + np.maximum(s_g, SD_FLOOR[k]) ** 2 / M)
             z = (m_g - m_r) / se
-            row.append(f"{k}: {np.mean(np.abs(z) <= 4.0):.4f} (max|z| {np.abs(z).max():.1f}, mean z {z.mean():+.3f})")
+            pop_r, pop_g = f[k + "_chains"], v.mean(1)
+            zp = (pop_g.mean() - pop_r.mean()) / np.sqrt(pop_r.var(ddof=1) / M_ref + pop_g.var(ddof=1) / M)
+            row.append(f"{k}: {np.mean(np.abs(z) <= 4.0):.4f} centred {np.mean(np.abs(z - z.mean()) <= 4.0):.4f} "
+                       f"(mean z {z.mean():+.2f}, pop z {zp:+.2f})")
         print(name, seed, " | ".join(row), flush=True)
