@@ -323,6 +323,60 @@ def test_sharded_path_bitwise_equals_unsharded(L, D, covs, n):
             sh.close()
 
 
+def test_full_size_c5_eight_shards_bitwise(L):
+    """Maximum size: the whole 10M-customer trivariate K=9 problem on one GPU, and
+    the same problem as the driver's 8-GPU layout — 8 shards of 1.25M customers through the
+    sharded C path on one card — agree bit for bit after 3 sweeps (state, summary sums, level-2
+    draws, log-likelihood): size-independent parity at the full c5 size (64-bit indexing, 39,063
+    blocks, 512-unit exchange)."""
+    import torch
+    from mcmc_clv_model_amd import distributed as Dm
+    from mcmc_clv_model_amd.data import synthetic_cbs
+    from mcmc_clv_model_amd.sampler import HipSampler, build_problem, make_prior
+    p = build_problem(synthetic_cbs(10_000_000, 9, 3, seed=20250719), [f"c{k}" for k in range(1, 9)], 3)
+    kw = dict(mcmc=2, burnin=1, thin=1, chains=1, seed=20250719, draw_sink="summary")
+    sweeps = 3
+    with HipSampler(p, **kw) as s:
+        s.run(sweeps)
+        ref = s.get_state()
+        ref_sums, k_ref = s.read_summary()
+        _, ref_l2, ref_ll = s.read_draws(level1=False)
+    assert k_ref == 2 and np.isfinite(ref_l2).all() and np.isfinite(ref_ll).all()
+    world = 8
+    plan = Dm.plan(p.N, world)
+    prior = make_prior(p, p.N)
+    shards = []
+    for r in range(world):
+        b, e = plan.shard(r)
+        shards.append(HipSampler(Dm.slice_problem(p, b, e), n_global=p.N, shard_begin=r * plan.blocks_per_rank * 256,
+                                 world_size=world, rank=r, blocks_per_rank=plan.blocks_per_rank,
+                                 blocks_per_unit=plan.blocks_per_unit, prior=prior, **kw))
+    nd = shards[0].partials()[1]
+    gathered = torch.zeros(nd * world, dtype=torch.float64, device="cuda")
+    try:
+        for _ in range(sweeps):  # trivariate: the level-2 draw closes each sweep
+            for sh in shards:
+                sh.sweep()
+            for r, sh in enumerate(shards):
+                sh.copy_partials(gathered.data_ptr() + r * nd * 8)
+                sh.synchronize()
+            for sh in shards:
+                sh.hyper(gathered.data_ptr())
+        for r, sh in enumerate(shards):
+            sh.synchronize()
+            b, e = plan.shard(r)
+            lam, mu, beta, sigma = sh.get_state()
+            assert np.array_equal(bits(lam), bits(ref[0][:, b:e])) and np.array_equal(bits(mu), bits(ref[1][:, b:e]))
+            assert np.array_equal(bits(beta), bits(ref[2])) and np.array_equal(bits(sigma), bits(ref[3]))
+            sums, _ = sh.read_summary()
+            assert np.array_equal(bits(sums), bits(ref_sums[:, :, b:e]))
+            _, l2, ll = sh.read_draws(level1=False)
+            assert np.array_equal(bits(l2), bits(ref_l2)) and np.array_equal(bits(ll), bits(ref_ll))
+    finally:
+        for sh in shards:
+            sh.close()
+
+
 @pytest.mark.parametrize("graph_chunk", [0, 4])
 def test_sharded_sampler_rccl_matches_fused(L, graph_chunk):
     """Row (e) through the production class: ShardedSampler at world size 1 over a real
