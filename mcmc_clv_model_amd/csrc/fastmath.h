@@ -102,4 +102,34 @@ __device__ __forceinline__ double exp_fast(double x, const double* lds_tab) {
   return __builtin_fma(ts, p, ts);
 }
 
+// exp_fast of two independent arguments, bit-identical to two exp_fast calls, written so that both
+// table reads are in flight before either is waited for: the compiler otherwise finishes the first
+// exp (table read, s_waitcnt, scaling) before starting the second, so the MH step's dependent chain
+// (both proposal exps, bi:299-301) paid the LDS latency twice.
+__device__ __forceinline__ void exp_fast2(double x1, double x2, const double* lds_tab, double& e1, double& e2) {
+  const double t1 = __builtin_fma(x1, EXP_INV_L, EXP_SHIFTER);
+  const double t2 = __builtin_fma(x2, EXP_INV_L, EXP_SHIFTER);
+  const int ki1 = (int)(uint32_t)__builtin_bit_cast(uint64_t, t1);
+  const int ki2 = (int)(uint32_t)__builtin_bit_cast(uint64_t, t2);
+  const double tab1 = lds_tab[ki1 & (EXP_TAB_N - 1)];
+  const double tab2 = lds_tab[ki2 & (EXP_TAB_N - 1)];
+  const double k1 = t1 - EXP_SHIFTER, k2 = t2 - EXP_SHIFTER;
+  double r1 = __builtin_fma(-k1, EXP_L_HI, x1), r2 = __builtin_fma(-k2, EXP_L_HI, x2);
+  r1 = __builtin_fma(-k1, EXP_L_LO, r1);
+  r2 = __builtin_fma(-k2, EXP_L_LO, r2);
+  double p1 = __builtin_fma(r1, 1.0 / 24.0, 1.0 / 6.0), p2 = __builtin_fma(r2, 1.0 / 24.0, 1.0 / 6.0);
+  p1 = __builtin_fma(p1, r1, 0.5);
+  p2 = __builtin_fma(p2, r2, 0.5);
+  p1 = __builtin_fma(p1, r1, 1.0);
+  p2 = __builtin_fma(p2, r2, 1.0);
+  p1 = p1 * r1;
+  p2 = p2 * r2;
+  uint64_t b1 = __builtin_bit_cast(uint64_t, tab1), b2 = __builtin_bit_cast(uint64_t, tab2);
+  b1 += (uint64_t)(int64_t)(ki1 >> 8) << 52;
+  b2 += (uint64_t)(int64_t)(ki2 >> 8) << 52;
+  const double s1 = __builtin_bit_cast(double, b1), s2 = __builtin_bit_cast(double, b2);
+  e1 = __builtin_fma(s1, p1, s1);
+  e2 = __builtin_fma(s2, p2, s2);
+}
+
 }  // namespace clv

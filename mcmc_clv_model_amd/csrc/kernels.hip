@@ -54,7 +54,9 @@ __device__ __forceinline__ double log_post_fast(const LPFast& c, double ll, doub
   const double t1 = __builtin_fma(c.A, ll, __builtin_fma(c.B, lm, c.Dl));
   const double t2 = __builtin_fma(c.C, lm, c.El);
   const double q = __builtin_fma(ll, t1, lm * t2);
-  return __builtin_fma(-c.w, exp_fast(ll, tab) + exp_fast(lm, tab), q);
+  double el, em;
+  exp_fast2(ll, lm, tab, el, em);  // = exp_fast(ll), exp_fast(lm), both table reads in flight
+  return __builtin_fma(-c.w, el + em, q);
 }
 
 // ---- wave-level reduce-scatter on CDNA4 cross-lane instructions ----
@@ -857,8 +859,13 @@ __device__ __forceinline__ void cust_ztau(Cust<D, K>& u, const SweepArgs& a, int
     if constexpr (REPLAY) uu = v_tau; else uu = u53(rz, rw);
     const double ml_tx = min700(ml * tx);
     const double ml_T = min700(ml * T);
-    const double e_tx = REPLAY ? exp(-ml_tx) : exp_fast(-ml_tx, exp_tab);  // both capped at 700 (bi:223)
-    const double e_T = REPLAY ? exp(-ml_T) : exp_fast(-ml_T, exp_tab);
+    double e_tx, e_T;  // both capped at 700 (bi:223)
+    if constexpr (REPLAY) {
+      e_tx = exp(-ml_tx);
+      e_T = exp(-ml_T);
+    } else {
+      exp_fast2(-ml_tx, -ml_T, exp_tab, e_tx, e_T);
+    }
     tau = -log((1 - uu) * e_tx + uu * e_T) / ml;
   }
   u.tau = tau;
@@ -1012,8 +1019,13 @@ __device__ __forceinline__ CustOut<D> cust_finish(Cust<D, K>& u, const SweepArgs
   const int64_t i = u.i;
   // bi:337-338 (state back to natural scale).  Replay reproduces the reference's exp/log round
   // trips (quirk Q5) bit for bit; Philox mode takes log(exp(ll)) = ll (equal to within an ulp).
-  double lam = REPLAY ? exp(u.ll) : exp_fast(u.ll, exp_tab);
-  double mu = REPLAY ? exp(u.lm) : exp_fast(u.lm, exp_tab);
+  double lam, mu;
+  if constexpr (REPLAY) {
+    lam = exp(u.ll);
+    mu = exp(u.lm);
+  } else {
+    exp_fast2(u.ll, u.lm, exp_tab, lam, mu);
+  }
   double eta = 1.0, Y[D];
   if constexpr (D == 3) {
     double m2 = 0.0;
