@@ -916,16 +916,31 @@ __device__ __forceinline__ void cust_prepare(Cust<D, K>& u, const SweepArgs& a, 
   cust_coeffs<D, K, REPLAY>(u, H, exp_tab);
 }
 
+// clip70(a * b + c) as three VALU ops: a VOP3 v_fma_f64 into a fresh register (the compiler
+// otherwise emits v_mov_b64 + v_fmac_f64, an accumulator copy, when c stays live) and v_max/v_min
+// written out too, so no NaN-canonicalising v_max is inserted after the asm (the operands are never
+// NaN).  Separate statements, so the scheduler interleaves the two coordinates' chains.
+__device__ __forceinline__ double clip70_fma(double a, double b, double c) {
+  double r, lo = -70.0, hi = 70.0;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(r), "v"(lo));
+  asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(r), "v"(hi));
+  return r;
+}
+
 // One Philox-mode MH step (bi:316-335) with lp(proposal) = -inf for pm > 5 (Q3): accept iff
-// pm <= 5 and exp(plp - cur) > u  <=>  plp - cur > log(u)  (cur = -inf accepts any finite one).
+// pm <= 5 and exp(plp - cur) > u  <=>  plp > cur + log(u)  (cur = -inf accepts any finite one;
+// cur + log u is formed off the dependent chain, alongside the proposal; a padded step's
+// log u = +inf gives +inf or NaN there, never accepted).
 template <int D, int K>
 __device__ __forceinline__ void mh_step(Cust<D, K>& u, double s00, double s11, float t_l, float t_m, float l_u,
                                         const double* exp_tab) {
-  const double pl = clip70(__builtin_fma(s00, (double)t_l, u.ll));
-  const double pm = clip70(__builtin_fma(s11, (double)t_m, u.lm));
+  const double thr = u.cur + (double)l_u;
+  const double pl = clip70_fma(s00, (double)t_l, u.ll);
+  const double pm = clip70_fma(s11, (double)t_m, u.lm);
   const double plp = log_post_fast(u.fc, pl, pm, exp_tab);
   // selects, not a branch: keeps a chunk's steps in one basic block with the next chunk's variates
-  const bool acc = (pm <= 5.0) & ((plp - u.cur) > (double)l_u);
+  const bool acc = (pm <= 5.0) & (plp > thr);
   u.ll = acc ? pl : u.ll;
   u.lm = acc ? pm : u.lm;
   u.cur = acc ? plp : u.cur;
