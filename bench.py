@@ -77,12 +77,15 @@ def committed_traffic(workload: str, sharded: bool, kname: str = "sweep_kernel")
     return best
 
 
-VALU_PEAK_WAVE_INSTS = 1024 * 2.4e9 / 4  # 256 CUs x 4 SIMDs, one wave64 fp64/int64 VALU op per 4 cycles
+N_SIMDS = 1024  # 256 CUs x 4 SIMDs (MI355X_MICROARCH.md)
+N_XCDS = 8      # GRBM_GUI_ACTIVE is summed over the 8 XCDs
 
 
-def committed_valu(workload: str, sharded: bool, kname: str = "sweep_kernel"):
-    """VALU wave-instructions per sweep-kernel launch (SQ_INSTS_VALU / SQ_WAVES x waves) from the
-    committed rocprofv3 summary of this workload; None if absent."""
+def committed_counters(workload: str, sharded: bool, kname: str = "sweep_kernel"):
+    """Counter evidence for the roofline's `bound` from the committed rocprofv3 summary of this
+    workload (tools/summarize_profile.py): VALU busy = SQ_ACTIVE_INST_VALU (quad-cycles, x4) summed
+    over the kernel's waves / (1,024 SIMDs x the dispatch's cycles, GRBM_GUI_ACTIVE / 8 XCDs) — the
+    share of SIMD cycles issuing VALU work — and the VALU-active share of the waves' lifetime."""
     import glob
     if sharded:
         return None
@@ -93,8 +96,12 @@ def committed_valu(workload: str, sharded: bool, kname: str = "sweep_kernel"):
         except Exception:
             continue
         for name, k in d.get("kernels", {}).items():
-            if kname in name and "valu_insts_per_wave" in k:
-                best = dict(wave_insts_per_sweep=k["valu_insts_per_wave"] * k["waves"] / k.get("sweeps_per_dispatch", 1),
+            if kname in name and "valu_active_quadcycles_per_wave" in k and k.get("grbm_gui_active"):
+                cycles = k["grbm_gui_active"] / N_XCDS
+                busy = 4.0 * k["valu_active_quadcycles_per_wave"] * k["waves"] / (N_SIMDS * cycles)
+                best = dict(valu_busy_frac=round(busy, 4),
+                            valu_active_frac_of_wave_lifetime=round(k["valu_active_frac_of_wave_lifetime"], 4),
+                            valu_insts_per_wave=round(k["valu_insts_per_wave"], 1), waves=k["waves"],
                             source=os.path.basename(path))
     return best
 
@@ -185,6 +192,63 @@ def cpu_baseline(workload: str, warm: int = 20, timed: int = 200):
     return res
 
 
+def measure_config(name: str, world: int, rank: int, local_rank: int, dist, steps: int, warmup: int,
+                   graph_chunk: int, exchange: str) -> dict:
+    """One BASELINE multi-GPU configuration at this world size: c4 = 1M bivariate
+    customers K=5 sharded over the ranks (strong scaling: the same problem at every N), c5 = 1.25M
+    trivariate customers K=9 per rank (weak scaling).  Wall time of `steps` sweeps (max over ranks)
+    after `warmup` sweeps; HBM fraction of the algorithmic bytes against N x 8 TB/s."""
+    import torch
+    from mcmc_clv_model_amd.sampler import HipSampler, build_problem
+    df, D, covs, chains, burnin, mcmc, thin, sink = load_workload(name, world)
+    n_total = len(df)
+    p = build_problem(df, covs, D)
+    del df
+    mcmc = max(mcmc, warmup + steps - burnin)
+    if world == 1:
+        kern = HipSampler(p, mcmc=mcmc, burnin=burnin, thin=thin, chains=chains, seed=42, draw_sink=sink,
+                          device=local_rank)
+        run, sync = kern.run, kern.synchronize
+    else:
+        from mcmc_clv_model_amd.distributed import ShardedSampler
+        kern = ShardedSampler(p, rank=rank, world=world, chains=chains, mcmc=mcmc, burnin=burnin, thin=thin, seed=42,
+                              draw_sink=sink, device=local_rank, graph_chunk=graph_chunk, exchange=exchange,
+                              verify_sweeps=8)
+        run, sync = kern.step, kern.synchronize
+    del p
+    run(warmup)
+    sync()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(steps)
+    sync()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    persistent = kern.launch_info()["persistent"]
+    exch = getattr(kern, "exchange", None)
+    note = getattr(kern, "p2p_note", None)
+    kern.close()
+    K = len(covs) + 1
+    value = chains * n_total * steps / dt
+    bpu = algorithmic_bytes(D, K, stored_fraction(burnin, thin, warmup + 1, warmup + steps), sink)
+    return dict(workload=f"{name}: {'bivariate' if D == 2 else 'trivariate'}, K={K}, synthetic "
+                         f"(mcmc_clv_model_amd.data.synthetic_cbs)",
+                scaling="strong" if name == "c4" else "weak", value=value, unit="customer-sweeps/s",
+                n_customers=n_total, customers_per_gpu=n_total // world, chains=chains, steps=steps, warmup=warmup,
+                ms_per_step=dt / steps * 1e3, draw_sink=sink,
+                hbm_frac=round(bpu * value / 1e9 / (world * HBM_PEAK_GBS), 5), bytes_per_unit=round(bpu, 2),
+                path=("persistent kernel" if persistent else "launch-per-sweep sweep kernel") +
+                     ("" if world == 1 else f", exchange {exch}" + (f" ({note})" if note else "")))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -202,6 +266,10 @@ def main():
                     help="world size > 1: unit-partial exchange per sweep — p2p = persistent kernel storing into "
                          "every rank's IPC-mapped mail over xGMI (auto: where it fits and verifies bitwise "
                          "against RCCL), rccl = all_gather per sweep")
+    ap.add_argument("--scaling-configs", default="c4,c5",
+                    help="BASELINE multi-GPU configurations also measured at this N (c4 strong, c5 weak "
+                         "scaling), reported under `configs`; '' to skip")
+    ap.add_argument("--scaling-steps", type=int, default=200)
     ap.add_argument("--cpu-baseline-child", action="store_true")
     ap.add_argument("--cpu-warm", type=int, default=20)
     ap.add_argument("--cpu-timed", type=int, default=200)
@@ -316,7 +384,7 @@ def main():
             units = chains * n_local * spl               # (chain, customer) sweeps per launch
             achieved = bpu * units / t_launch / 1e9
             kname = "persist_kernel" if persistent else "sweep_kernel"
-            roofline = dict(bound="hbm", achieved=round(achieved, 3), peak=HBM_PEAK_GBS, unit="GB/s",
+            roofline = dict(bound=None, achieved=round(achieved, 3), peak=HBM_PEAK_GBS, unit="GB/s",
                             frac=round(achieved / HBM_PEAK_GBS, 6), traffic=None,
                             kernel=("persist_kernel (one launch for all sweeps of a clv_run; level-2 workgroup "
                                     "per chain" + ("; unit partials exchanged over xGMI" if p2p else "") + ")")
@@ -333,13 +401,26 @@ def main():
                 roofline["traffic_source"] = f"{tr['source']}: {tr['counters']}"
             if kt["hyper_launches"]:
                 roofline["hyper_kernel_us"] = round(kt["hyper_ms"] / kt["hyper_launches"] * 1e3, 3)
-            v = committed_valu(a.workload, sharded and not p2p, kname)
-            if v:  # the binding resource: VALU issue, not HBM
-                ach = v["wave_insts_per_sweep"] / t_sweep
-                roofline["valu"] = dict(achieved=round(ach / 1e9, 2), peak=round(VALU_PEAK_WAVE_INSTS / 1e9, 1),
-                                        unit="G wave-instructions/s", frac=round(ach / VALU_PEAK_WAVE_INSTS, 4),
-                                        source=v["source"],
-                                        note="peak = 1,024 SIMDs x 2.4 GHz / 4 cycles (fp64-rate VALU issue)")
+            # bound: from the counters (HBM traffic rate vs peak, VALU busy share), not assumed
+            ev = committed_counters(a.workload, sharded and not p2p, kname) or {}
+            if roofline["traffic"] is not None:
+                ev["hbm_traffic_frac"] = round(roofline["traffic"] / t_launch / 1e9 / HBM_PEAK_GBS, 4)
+            if ev.get("hbm_traffic_frac", 0.0) >= 0.6:
+                roofline["bound"] = "hbm"
+            elif ev.get("valu_busy_frac", 0.0) >= 0.7:
+                roofline["bound"] = "valu"
+            elif "valu_busy_frac" in ev:
+                roofline["bound"] = "latency"
+            else:
+                roofline["bound"] = "unmeasured"
+            ev["rule"] = "hbm if measured HBM traffic >= 0.6 of peak; else valu if VALU busy >= 0.7; else latency"
+            roofline["bound_evidence"] = ev
+
+    kern.close()
+    extra = {}
+    for name in [c for c in a.scaling_configs.split(",") if c]:
+        extra[name] = measure_config(name, world, rank, local_rank, dist, a.scaling_steps, 20, a.graph_chunk,
+                                     a.exchange if world > 1 else "rccl")
 
     if rank == 0:
         cpu = None
@@ -350,6 +431,7 @@ def main():
             metric="MCMC sweeps/sec x N_customers (customer-sweeps/s)", value=value, unit="customer-sweeps/s",
             n_gpus=world, steps=a.steps, warmup=a.warmup, ms_per_step=dt / a.steps * 1e3, higher_is_better=True,
             scaling="weak", vs_baseline=None, dtype="f64",
+            proposal_dtype="f32",  # t3 proposal noise and accept log-uniforms; state, posterior f64
             data=(f"synthetic CBS ({n_total} customers, mcmc_clv_model_amd.data.synthetic_cbs)"
                   if WORKLOADS[a.workload][1].startswith("synthetic:") else
                   (f"CDNOW {WORKLOADS[a.workload][1]} CBS ({n_total // world:,} real customers, "
@@ -368,9 +450,9 @@ def main():
             exchange=(None if world == 1 and not sharded else
                       dict(kind=kern.exchange, note=kern.p2p_note, requested=a.exchange if world > 1 else "rccl")),
             speedup_vs_cpu_1core=(value / cpu["value"]) if cpu else None,
+            configs=extra or None,
         )
         print(json.dumps(line))
-    kern.close()
     if dist:
         dist.destroy_process_group()
 

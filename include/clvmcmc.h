@@ -120,6 +120,10 @@ int64_t clv_replay_sweep_stride(const clv_sampler* s);
  * tau (bi:390), level-2 (bi:393), level-1 MH (bi:396), eta (tri:524-526), storage (bi:402-428).
  * Synchronous; chunks of sweeps are replayed from a captured hipGraph. */
 int clv_run(clv_sampler* s, int64_t n_sweeps);
+/* Persistent path only: undo the last completed clv_run (state, sweep count, summary sums) — a
+ * sharded step whose persistent launch failed on another rank is redone by every rank from the
+ * same point.  A clv_run that fails (a wait timed out) already leaves the state unchanged. */
+int clv_rollback(clv_sampler* s);
 
 /* Sharded stepping (one process per GPU; the caller exchanges the unit partials over RCCL):
  *   after clv_create, bivariate only: [exchange] clv_hyper   (initial draw, bi:393 of sweep 1)
@@ -153,7 +157,10 @@ int clv_launch_info(const clv_sampler* s, int64_t* out);
  *                    pointers valid in this process (ranks sharing one process).  Collective in
  *                    effect: call it on every rank, then barrier, before the first clv_run.
  * After connecting, clv_run(n) runs n sweeps (bivariate: after the initial clv_hyper); every rank
- * must call it with the same n (a rank that waits > 2 s for its peers fails with CLV_EHIP). */
+ * must call it with the same n.  A rank that waits longer than the bound (10 s by default,
+ * CLV_WAIT_TIMEOUT_MS) for its peers fails with CLV_EHIP and keeps its state from before the call;
+ * ranks whose call completed undo it with clv_rollback, and clv_p2p_connect may be called again
+ * (it refills this rank's mail) to resume the peer exchange. */
 #define CLV_IPC_HANDLE_BYTES 64
 int clv_p2p_info(const clv_sampler* s, int64_t* out);
 int clv_p2p_export(clv_sampler* s, void* handle);
@@ -209,6 +216,16 @@ int clv_debug_hyper_variates(uint64_t seed, int32_t chain, uint32_t sweep, doubl
                              double* chi2, double* normals);
 /* The Philox-mode MH step's fp64 exp (csrc/fastmath.h, |x| <= 700) on n values. */
 int clv_debug_exp(const double* x, int64_t n, double* out);
+/* One Philox-mode MH step exactly as the sweep kernels run it (bi:291-335: log posterior with the
+ * Q3 cap, fma + clip proposal, accept iff pm <= 5 and plp > cur + log U), on n independent lanes.
+ * Per lane: x, z, T_cal, tau, mean [n][2] (X @ beta), cur_pt [n][2] (log lambda, log mu), t3 [n][2]
+ * (fp32 t3 noise), log_u (fp32, +inf = a padded step); shared prec3 = inv(Sigma)[0:2,0:2] as
+ * (p00, p01, p11) and scale2 = (Sigma00, Sigma11) (Q2).  out [n][7] = current log posterior (up
+ * to a per-customer constant), the proposal's (before the Q3 cap), the proposal (pl, pm), the new
+ * log lambda, log mu and log posterior. */
+int clv_debug_mh_step(int64_t n, const int32_t* x, const uint8_t* z, const double* T_cal, const double* tau,
+                      const double* mean, const double* prec3, const double* cur_pt, const float* t3,
+                      const double* scale2, const float* log_u, double* out);
 /* Host only (no device): the persistent grid's placement map for n_chains chains of nb customer
  * workgroups (+1 level-2 workgroup each) on n_cu CUs — out[linear workgroup] = chain << 16 | block. */
 int clv_debug_wg_map(int32_t n_chains, int32_t nb, int32_t n_cu, int32_t* out);

@@ -86,6 +86,7 @@ def lib() -> ctypes.CDLL:
         "clv_set_replay_tape": (c_int32, [sp, dp, c_int64]),
         "clv_replay_sweep_stride": (c_int64, [sp]),
         "clv_run": (c_int32, [sp, c_int64]),
+        "clv_rollback": (c_int32, [sp]),
         "clv_sweep": (c_int32, [sp]),
         "clv_hyper": (c_int32, [sp, c_void_p]),
         "clv_partials": (c_int32, [sp, POINTER(c_void_p), POINTER(c_int64), POINTER(c_int32)]),
@@ -112,6 +113,8 @@ def lib() -> ctypes.CDLL:
         "clv_debug_stamps": (c_int32, [sp, POINTER(c_uint64)]),
         "clv_debug_wg_stamps": (c_int32, [sp, POINTER(c_uint64)]),
         "clv_debug_exp": (c_int32, [dp, c_int64, dp]),
+        "clv_debug_mh_step": (c_int32, [c_int64, POINTER(c_int32), POINTER(c_uint8), dp, dp, dp, dp, dp,
+                                        POINTER(c_float), dp, POINTER(c_float), dp]),
         "clv_debug_wg_map": (c_int32, [c_int32, c_int32, c_int32, POINTER(c_int32)]),
         "clv_predict": (c_int32, [c_int32, dp, c_int64, c_int64, c_int32, dp, c_double, c_uint64, c_int32, c_double,
                                   POINTER(c_int64), dp]),

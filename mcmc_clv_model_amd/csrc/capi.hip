@@ -70,6 +70,11 @@ SweepArgs sweep_args(clv_sampler* s, int init, int fuse = 0) {
   a.peers = s->d_peers;
   a.wg_map = s->d_wgmap;
   a.rank = s->cfg.rank;
+  a.lam_out = s->d_lam_alt ? s->d_lam_alt : s->d_lam;
+  a.mu_out = s->d_mu_alt ? s->d_mu_alt : s->d_mu;
+  a.hyper_out = s->d_hyper_alt ? s->d_hyper_alt : s->d_hyper;
+  a.wait_ticks = s->wait_ticks;
+  a.abort_host = s->d_h_abort;
   {  // CLV_PRE_VARIATES=0: draw the MH variates inside the MH phase (A/B measurements)
     const char* env = std::getenv("CLV_PRE_VARIATES");
     a.pre_variates = (env && std::string(env) == "0") ? 0 : 1;
@@ -106,6 +111,8 @@ HyperArgs hyper_args(clv_sampler* s, const double* units, int mode) {
 }
 
 int enqueue_sweep(clv_sampler* s, hipEvent_t e0, hipEvent_t e1) {
+  s->slots_dirty = true;  // block partials written (the persistent hand-off needs its sentinel fill)
+  s->last_persist_n = 0;
   CLV_HIP(launch_sweep(sweep_args(s, 0), s->replay, s->stream, e0, e1));
   if (s->g.blocks_per_unit > 1) {
     GroupArgs ga{};
@@ -119,11 +126,14 @@ int enqueue_sweep(clv_sampler* s, hipEvent_t e0, hipEvent_t e1) {
 
 // world_size == 1: one launch per sweep (the level-2 draw runs in the sweep kernel's tail)
 int enqueue_fused(clv_sampler* s, hipEvent_t e0, hipEvent_t e1) {
+  s->slots_dirty = true;
+  s->last_persist_n = 0;
   CLV_HIP(launch_sweep(sweep_args(s, 0, 1), s->replay, s->stream, e0, e1));
   return CLV_OK;
 }
 
 int enqueue_hyper(clv_sampler* s, const double* units, int mode, hipEvent_t e0, hipEvent_t e1) {
+  s->last_persist_n = 0;
   if (e0) CLV_HIP(hipEventRecord(e0, s->stream));
   CLV_HIP(launch_hyper(hyper_args(s, units, mode), s->replay, s->stream));
   if (e1) CLV_HIP(hipEventRecord(e1, s->stream));
@@ -418,6 +428,21 @@ int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* pri
       CLV_HIPC(dalloc(&s->d_peers, g.world_size));
     }
   }
+  if (s->persistent || s->p2p_capable) {
+    CLV_HIPC(dalloc(&s->d_lam_alt, C * std::max<int64_t>(n, 1)));
+    CLV_HIPC(dalloc(&s->d_mu_alt, C * std::max<int64_t>(n, 1)));
+    CLV_HIPC(dalloc(&s->d_hyper_alt, C * HS));
+    if (cfg->draw_sink == CLV_SINK_SUMMARY && n > 0) CLV_HIPC(dalloc(&s->d_sums_prev, (size_t)C * CLV_N_SUM_STATS * n));
+    CLV_HIPC(hipHostMalloc((void**)&s->h_abort, sizeof(uint32_t), hipHostMallocMapped));
+    *s->h_abort = 0;
+    CLV_HIPC(hipHostGetDevicePointer((void**)&s->d_h_abort, s->h_abort, 0));
+    // every wait of the persistent kernel is bounded: 2 s at world size 1 (all workgroups are
+    // resident, so a wait that long means a fault), 10 s with peers (host-side launch skew between
+    // ranks); CLV_WAIT_TIMEOUT_MS overrides
+    const char* env = std::getenv("CLV_WAIT_TIMEOUT_MS");
+    const double ms = env ? std::atof(env) : (cfg->world_size > 1 ? 10000.0 : 2000.0);
+    s->wait_ticks = (uint64_t)(std::max(1.0, ms) * 1e5);  // s_memrealtime: 100 MHz
+  }
   if ((s->persistent || s->p2p_capable) && s->n_cu > 0) {
     // default on for the bivariate model only: measured c2 13.44 -> 12.94 us per sweep, but c3
     // (trivariate: longer level-2 draw, so both waves of a same-chain pair idle in the hand-off
@@ -524,6 +549,9 @@ void clv_destroy(clv_sampler* s) {
     if (p) (void)hipFree(p);
   if (s->d_unit && s->d_unit != s->d_block) (void)hipFree(s->d_unit);
   if (s->d_hyp2) (void)hipFree(s->d_hyp2);
+  for (void* p : {(void*)s->d_lam_alt, (void*)s->d_mu_alt, (void*)s->d_hyper_alt, (void*)s->d_sums_prev})
+    if (p) (void)hipFree(p);
+  if (s->h_abort) (void)hipHostFree(s->h_abort);
   for (void* p : s->ipc_opened) (void)hipIpcCloseMemHandle(p);
   if (s->d_mail) (void)hipFree(s->d_mail);
   if (s->d_peers) (void)hipFree(s->d_peers);
@@ -643,8 +671,18 @@ int clv_p2p_export(clv_sampler* s, void* handle) {
 int clv_p2p_connect(clv_sampler* s, const void* handles, const uint64_t* ptrs) {
   if (!s || (!handles && !ptrs)) return fail(CLV_EINVAL, "null argument");
   if (!s->p2p_capable) return fail(CLV_ESTATE, "no peer exchange for this geometry (grid does not fit at once)");
-  if (s->p2p_ready) return fail(CLV_ESTATE, "already connected");
   CLV_HIP(hipSetDevice(s->device));
+  CLV_HIP(hipStreamSynchronize(s->stream));
+  if (s->p2p_ready || !s->ipc_opened.empty()) {  // reconnect (after a failed step): drop the old mappings
+    s->p2p_ready = false;
+    for (void* p : s->ipc_opened) (void)hipIpcCloseMemHandle(p);
+    s->ipc_opened.clear();
+  }
+  {  // every slot of this rank's mail empty (a failed step may have left units of any rank there);
+     // the caller synchronises the ranks after connecting, before any rank runs
+    const int64_t nm = 2LL * s->g.world_size * s->g.n_chains * s->g.stride * s->g.units_per_rank;
+    CLV_HIP(hipMemsetAsync(s->d_mail, 0xFF, sizeof(double) * nm, s->stream));
+  }
   const int W = s->g.world_size, r = s->cfg.rank;
   std::vector<double*> peers(W, nullptr);
   for (int q = 0; q < W; ++q) {
@@ -663,7 +701,7 @@ int clv_p2p_connect(clv_sampler* s, const void* handles, const uint64_t* ptrs) {
     if (!peers[q]) return fail(CLV_EINVAL, "null peer mail pointer");
   }
   CLV_HIP(hipMemcpy(s->d_peers, peers.data(), sizeof(double*) * W, hipMemcpyHostToDevice));
-  CLV_HIP(hipStreamSynchronize(s->stream));  // the mail's sentinel fill (create) has landed
+  CLV_HIP(hipStreamSynchronize(s->stream));  // the mail's sentinel fill has landed
   s->p2p_ready = true;
   return CLV_OK;
 }
@@ -681,6 +719,7 @@ int clv_set_stream(clv_sampler* s, uint64_t stream) {
 int clv_note_sweeps(clv_sampler* s, int64_t n) {
   if (!s || s->sweeps_done + n < 0) return fail(CLV_EINVAL, "bad arguments");
   s->sweeps_done += n;
+  s->last_persist_n = 0;
   return CLV_OK;
 }
 
@@ -688,12 +727,20 @@ namespace {
 // Persistent path: one launch of persist_kernel for all n sweeps (see kernels.hip).
 int run_persistent(clv_sampler* s, int64_t n_sweeps) {
   if (n_sweeps == 0) return CLV_OK;
-  // every hand-off slot empty (all-ones bytes: the sentinel NaN)
-  CLV_HIP(hipMemsetAsync(s->d_hyp2, 0xFF, sizeof(double) * 2 * s->g.n_chains * HS, s->stream));
-  // (only the nb_local live columns of each [chain][stat] row: padding blocks stay 0.0 for the
-  // group kernel of the sharded path)
-  CLV_HIP(hipMemset2DAsync(s->d_block, sizeof(double) * s->g.blocks_per_rank, 0xFF, sizeof(double) * s->g.nb_local,
-                           (size_t)s->g.n_chains * s->g.stride, s->stream));
+  const Geometry& g = s->g;
+  s->last_persist_n = 0;
+  if (s->slots_dirty) {  // a completed launch leaves every hand-off slot empty; else fill them
+    // every hand-off slot empty (all-ones bytes: the sentinel NaN)
+    CLV_HIP(hipMemsetAsync(s->d_hyp2, 0xFF, sizeof(double) * 2 * g.n_chains * HS, s->stream));
+    // (only the nb_local live columns of each [chain][stat] row: padding blocks stay 0.0 for the
+    // group kernel of the sharded path)
+    CLV_HIP(hipMemset2DAsync(s->d_block, sizeof(double) * g.blocks_per_rank, 0xFF, sizeof(double) * g.nb_local,
+                             (size_t)g.n_chains * g.stride, s->stream));
+    s->slots_dirty = false;
+  }
+  const size_t sums_bytes = sizeof(double) * (size_t)g.n_chains * CLV_N_SUM_STATS * g.n;
+  if (s->d_sums_prev)  // an aborted (or rolled-back) launch restores the running sums from here
+    CLV_HIP(hipMemcpyAsync(s->d_sums_prev, s->d_sums, sums_bytes, hipMemcpyDeviceToDevice, s->stream));
   SweepArgs a = sweep_args(s, 0, 1);
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (s->timing) {
@@ -711,16 +758,31 @@ int run_persistent(clv_sampler* s, int64_t n_sweeps) {
     if (rc) return rc;
   }
   CLV_HIP(hipStreamSynchronize(s->stream));
-  uint32_t ab = 0;
-  CLV_HIP(hipMemcpy(&ab, &s->d_ctrl->abort, sizeof(uint32_t), hipMemcpyDeviceToHost));
-  if (ab) {
-    (void)hipMemset(&s->d_ctrl->abort, 0, sizeof(uint32_t));
-    if (s->g.world_size > 1) s->p2p_ready = false;  // mail slots are in an unknown state now
-    return fail(CLV_EHIP, s->g.world_size > 1
-                              ? "persistent sweep kernel: a wait exceeded 2 s (a peer rank not running, or not all resident?)"
-                              : "persistent sweep kernel: a workgroup waited > 2 s for its chain (not all resident?)");
+  if (__atomic_load_n(s->h_abort, __ATOMIC_ACQUIRE)) {
+    // the carried state was written to the *_alt buffers only: lam / mu / hyper still hold the
+    // state this launch started from; restore the counters, flags and running sums
+    *s->h_abort = 0;
+    Ctrl c{};
+    c.cur = s->sweeps_done;
+    CLV_HIP(hipMemcpy(s->d_ctrl, &c, sizeof(Ctrl), hipMemcpyHostToDevice));
+    if (s->d_sums_prev) CLV_HIP(hipMemcpy(s->d_sums, s->d_sums_prev, sums_bytes, hipMemcpyDeviceToDevice));
+    s->slots_dirty = true;
+    if (g.world_size > 1) s->p2p_ready = false;  // mail slots are in an unknown state now
+    return fail(CLV_EHIP, g.world_size > 1
+                              ? "persistent sweep kernel: a wait timed out (a peer rank not running, or not all resident?); "
+                                "state unchanged"
+                              : "persistent sweep kernel: a workgroup timed out waiting for its chain (not all resident?); "
+                                "state unchanged");
+  }
+  std::swap(s->d_lam, s->d_lam_alt);
+  std::swap(s->d_mu, s->d_mu_alt);
+  std::swap(s->d_hyper, s->d_hyper_alt);
+  if (s->graph_exec) {  // captured with the previous state pointers
+    CLV_HIP(hipGraphExecDestroy(s->graph_exec));
+    s->graph_exec = nullptr;
   }
   s->sweeps_done += n_sweeps;
+  s->last_persist_n = n_sweeps;
   return CLV_OK;
 }
 }  // namespace
@@ -780,6 +842,29 @@ int clv_run(clv_sampler* s, int64_t n_sweeps) {
     }
   }
   CLV_HIP(hipStreamSynchronize(s->stream));
+  return CLV_OK;
+}
+
+int clv_rollback(clv_sampler* s) {
+  if (!s) return fail(CLV_EINVAL, "null sampler");
+  if (s->last_persist_n <= 0) return fail(CLV_ESTATE, "nothing to roll back (the last call was not a completed persistent clv_run)");
+  CLV_HIP(hipSetDevice(s->device));
+  CLV_HIP(hipStreamSynchronize(s->stream));
+  std::swap(s->d_lam, s->d_lam_alt);
+  std::swap(s->d_mu, s->d_mu_alt);
+  std::swap(s->d_hyper, s->d_hyper_alt);
+  s->sweeps_done -= s->last_persist_n;
+  s->last_persist_n = 0;
+  Ctrl c{};
+  c.cur = s->sweeps_done;
+  CLV_HIP(hipMemcpy(s->d_ctrl, &c, sizeof(Ctrl), hipMemcpyHostToDevice));
+  if (s->d_sums_prev)
+    CLV_HIP(hipMemcpy(s->d_sums, s->d_sums_prev, sizeof(double) * (size_t)s->g.n_chains * CLV_N_SUM_STATS * s->g.n,
+                      hipMemcpyDeviceToDevice));
+  if (s->graph_exec) {
+    CLV_HIP(hipGraphExecDestroy(s->graph_exec));
+    s->graph_exec = nullptr;
+  }
   return CLV_OK;
 }
 
@@ -854,6 +939,7 @@ int clv_set_state(clv_sampler* s, const double* lambdas, const double* mus, cons
   CLV_HIP(hipMemcpyAsync(s->d_ctrl, &c, sizeof(Ctrl), hipMemcpyHostToDevice, s->stream));
   CLV_HIP(hipStreamSynchronize(s->stream));
   s->sweeps_done = sweeps_done;
+  s->last_persist_n = 0;
   return CLV_OK;
 }
 
@@ -862,6 +948,11 @@ int clv_set_timing(clv_sampler* s, int32_t enable) {
   int rc = harvest_timing(s);  // never drop pending timed launches
   if (rc) return rc;
   s->timing = enable != 0;
+  if (s->timing) {  // created here, not inside the first timed clv_run
+    CLV_HIP(hipSetDevice(s->device));
+    rc = ensure_events(s);
+    if (rc) return rc;
+  }
   s->t_sweep_ms = s->t_hyper_ms = 0.0;
   s->n_sweep_timed = s->n_hyper_timed = 0;
   return CLV_OK;
@@ -989,6 +1080,44 @@ int clv_debug_wg_map(int32_t n_chains, int32_t nb, int32_t n_cu, int32_t* out) {
     return fail(CLV_EINVAL, "bad arguments");
   const std::vector<int32_t> m = persist_wg_map(n_chains, nb, n_cu);
   std::copy(m.begin(), m.end(), out);
+  return CLV_OK;
+}
+
+int clv_debug_mh_step(int64_t n, const int32_t* x, const uint8_t* z, const double* T_cal, const double* tau,
+                      const double* mean, const double* prec3, const double* cur_pt, const float* t3,
+                      const double* scale2, const float* log_u, double* out) {
+  if (!x || !z || !T_cal || !tau || !mean || !prec3 || !cur_pt || !t3 || !scale2 || !log_u || !out || n < 1)
+    return fail(CLV_EINVAL, "bad arguments");
+  int32_t *dx;
+  uint8_t* dz;
+  double *dT, *dtau, *dm, *dp, *dc, *ds, *dout;
+  float *dt3, *dlu;
+  CLV_HIP(hipMalloc(&dx, sizeof(int32_t) * n));
+  CLV_HIP(hipMalloc(&dz, n));
+  CLV_HIP(dalloc(&dT, n));
+  CLV_HIP(dalloc(&dtau, n));
+  CLV_HIP(dalloc(&dm, 2 * n));
+  CLV_HIP(dalloc(&dp, 3));
+  CLV_HIP(dalloc(&dc, 2 * n));
+  CLV_HIP(dalloc(&ds, 2));
+  CLV_HIP(dalloc(&dout, 7 * n));
+  CLV_HIP(hipMalloc(&dt3, sizeof(float) * 2 * n));
+  CLV_HIP(hipMalloc(&dlu, sizeof(float) * n));
+  CLV_HIP(hipMemcpy(dx, x, sizeof(int32_t) * n, hipMemcpyHostToDevice));
+  CLV_HIP(hipMemcpy(dz, z, n, hipMemcpyHostToDevice));
+  CLV_HIP(hipMemcpy(dT, T_cal, sizeof(double) * n, hipMemcpyHostToDevice));
+  CLV_HIP(hipMemcpy(dtau, tau, sizeof(double) * n, hipMemcpyHostToDevice));
+  CLV_HIP(hipMemcpy(dm, mean, sizeof(double) * 2 * n, hipMemcpyHostToDevice));
+  CLV_HIP(hipMemcpy(dp, prec3, sizeof(double) * 3, hipMemcpyHostToDevice));
+  CLV_HIP(hipMemcpy(dc, cur_pt, sizeof(double) * 2 * n, hipMemcpyHostToDevice));
+  CLV_HIP(hipMemcpy(ds, scale2, sizeof(double) * 2, hipMemcpyHostToDevice));
+  CLV_HIP(hipMemcpy(dt3, t3, sizeof(float) * 2 * n, hipMemcpyHostToDevice));
+  CLV_HIP(hipMemcpy(dlu, log_u, sizeof(float) * n, hipMemcpyHostToDevice));
+  CLV_HIP(launch_debug_mh(dx, dz, dT, dtau, dm, dp, dc, dt3, ds, dlu, n, dout, nullptr));
+  CLV_HIP(hipMemcpy(out, dout, sizeof(double) * 7 * n, hipMemcpyDeviceToHost));
+  for (void* p : {(void*)dx, (void*)dz, (void*)dT, (void*)dtau, (void*)dm, (void*)dp, (void*)dc, (void*)ds,
+                  (void*)dout, (void*)dt3, (void*)dlu})
+    CLV_HIP(hipFree(p));
   return CLV_OK;
 }
 

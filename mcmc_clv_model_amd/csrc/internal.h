@@ -74,6 +74,17 @@ struct clv_sampler {
   clv::Ctrl* d_ctrl = nullptr;
   uint32_t* d_arrive = nullptr;     // fused-tail arrival counters: [chain], then [chain][units_per_rank]
   double* d_hyp2 = nullptr;         // persistent kernel: [2][chain][HS] hand-off slots
+  // persistent kernel: the launch writes its carried state into the *_alt buffers; clv_run swaps
+  // them in only when no wave aborted (an aborted launch leaves the state untouched), and
+  // clv_rollback swaps them back (a sharded step that failed on another rank)
+  double *d_lam_alt = nullptr, *d_mu_alt = nullptr, *d_hyper_alt = nullptr;
+  double* d_sums_prev = nullptr;    // summary sink: the running sums before the last persistent launch
+  uint32_t* h_abort = nullptr;      // host-mapped copy of ctrl->abort (the kernel stores it on a timeout)
+  uint32_t* d_h_abort = nullptr;    // its device address
+  uint64_t wait_ticks = 0;          // bound on every persistent-kernel wait (s_memrealtime ticks)
+  bool slots_dirty = true;          // hand-off slots need the sentinel fill (a completed persistent
+                                    // launch leaves them empty; sweep kernels write block partials)
+  int64_t last_persist_n = 0;       // sweeps of the last persistent launch (rollback), 0 = none
   bool persistent = false;          // clv_run uses persist_kernel (all workgroups resident)
   int persist_bpc = 0, n_cu = 0;    // persist_kernel occupancy (workgroups per CU), CUs
   // world size > 1: persistent kernel with the peer (xGMI) exchange

@@ -108,6 +108,14 @@ struct SweepArgs {
   int rank;
   const int32_t* wg_map;     // persistent kernel: linear workgroup -> (chain << 16 | block), or null
   int pre_variates;          // persistent kernel: draw the next sweep's MH variates during the hand-off
+  // persistent kernel: the carried state at the end of a launch goes to these (the host swaps them
+  // with lam / mu / hyper only if no wave aborted), the bound on every wait (s_memrealtime ticks,
+  // 100 MHz) and a host-mapped copy of ctrl->abort (read by the host after the launch, no D2H copy)
+  double* lam_out;
+  double* mu_out;
+  double* hyper_out;
+  uint64_t wait_ticks;
+  uint32_t* abort_host;
   HyperArgs h;               // level-2 arguments of the fused tail
   unsigned long long* stamps; // diagnostic build only (CLV_STAMPS): [1024][8] s_memrealtime stamps
 };
@@ -139,5 +147,8 @@ hipError_t launch_debug_level2(int D, int K, const double* prior_dev, const doub
 hipError_t launch_debug_hyper_variates(uint64_t seed, int chain, uint32_t sweep, double df, int64_t n,
                                        double* chi2, double* normals, hipStream_t st);
 hipError_t launch_debug_exp(const double* x, int64_t n, double* out, hipStream_t st);
+hipError_t launch_debug_mh(const int32_t* x, const uint8_t* z, const double* T, const double* tau, const double* m,
+                           const double* prec, const double* cur_pt, const float* t3, const double* scale,
+                           const float* log_u, int64_t n, double* out, hipStream_t st);
 
 }  // namespace clv

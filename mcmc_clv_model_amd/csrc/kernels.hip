@@ -1367,10 +1367,12 @@ __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
 // after seeing that.  (beta, Sigma): two slot sets by sweep parity; set s&1 is reset (after all
 // readers of s have delivered their partials) before the set of s+1 is written, so a reader of
 // s+2 sees the reset or newer.  Sums are formed in the fused path's order: results are bitwise
-// identical to the launch-per-sweep path.  Every wait is bounded (PERSIST_TIMEOUT): a wave that
-// times out raises ctrl->abort and every wave leaves at its next wait.
+// identical to the launch-per-sweep path.  Every wait is bounded (SweepArgs::wait_ticks, 2 s by
+// default): a wave that times out raises ctrl->abort (and the host-mapped copy the host reads after
+// the launch) and every wave leaves at its next wait.  The carried state (lambda, mu, hyper) is
+// written to the *_out buffers, which the host adopts only when no wave aborted: an aborted launch
+// leaves the state it started from untouched.
 // ---------------------------------------------------------------------------------------------
-constexpr uint64_t PERSIST_TIMEOUT = 200000000ull;  // s_memrealtime ticks (100 MHz): 2 s
 constexpr long long SLOT_EMPTY = -1ll;              // all-ones bit pattern: a NaN no arithmetic yields
 
 __device__ __forceinline__ double ld_wt(const double* p) {
@@ -1391,10 +1393,12 @@ __device__ __forceinline__ double slot_empty() { return __longlong_as_double(SLO
 
 // Bounded wait bookkeeping (uniform): true when this wave must give up.  The abort flag is read
 // every 16th poll only, so a poll iteration costs one memory round trip, not two.
-__device__ __forceinline__ bool wait_expired(uint64_t t0, Ctrl* ctrl, uint32_t poll) {
-  if ((poll & 15u) == 15u && __hip_atomic_load(&ctrl->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return true;
-  if (__builtin_amdgcn_s_memrealtime() - t0 > PERSIST_TIMEOUT) {
-    __hip_atomic_store(&ctrl->abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ bool wait_expired(const SweepArgs& a, uint64_t t0, uint32_t poll) {
+  if ((poll & 15u) == 15u && __hip_atomic_load(&a.ctrl_rw->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+    return true;
+  if (__builtin_amdgcn_s_memrealtime() - t0 > a.wait_ticks) {
+    __hip_atomic_store(&a.ctrl_rw->abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (a.abort_host) __hip_atomic_store(a.abort_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     return true;
   }
   return false;
@@ -1492,7 +1496,7 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
           }
         }
         if (__all(done)) break;
-        if (wait_expired(t0, a.ctrl_rw, poll)) {
+        if (wait_expired(a, t0, poll)) {
           s_abort = 1;
           break;
         }
@@ -1574,7 +1578,7 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
           mdone = ok;
         }
         if (__all(mdone)) break;
-        if (wait_expired(tw, a.ctrl_rw, poll)) {
+        if (wait_expired(a, tw, poll)) {
           s_abort = 1;
           break;
         }
@@ -1629,7 +1633,7 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
     // 6. publish (beta, Sigma) of sweep s+1: one coalesced write-through store per lane
     const bool last = it == n_sweeps - 1;
     if (tid < HS) {
-      if (last) a.h.hyper[(int64_t)c * HS + tid] = Hs[tid];  // the carried state (kernel boundary)
+      if (last) a.hyper_out[(int64_t)c * HS + tid] = Hs[tid];  // the carried state (kernel boundary)
       else st_wt(a.hyp2 + ((int64_t)((s + 1) & 1) * g.n_chains + c) * HS + tid, Hs[tid]);
     }
     CLV_P_STAMP(a.stamps, wgi, 4, stp);
@@ -1727,7 +1731,7 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
             Hs[tid] = v;
             break;
           }
-          if (wait_expired(t0, a.ctrl_rw, poll)) {
+          if (wait_expired(a, t0, poll)) {
             if (tid == 0) s_abort = 1;
             break;
           }
@@ -1770,10 +1774,10 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
     }
     CLV_P_STAMP(a.stamps, wgi, 6, stp);
   }
-  if (cu.active) {  // the carried state, once per launch
+  if (cu.active) {  // the carried state, once per launch (adopted by the host if nothing aborted)
     const int64_t ci = (int64_t)c * g.n + cu.i;
-    a.lam[ci] = cu.lam;
-    a.mu[ci] = cu.mu;
+    a.lam_out[ci] = cu.lam;
+    a.mu_out[ci] = cu.mu;
   }
 }
 
@@ -1864,6 +1868,52 @@ __global__ void debug_exp_kernel(const double* x, int64_t n, double* out) {
   __syncthreads();
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) out[i] = exp_fast(x[i], tab);
+}
+
+// The shipped Philox-mode MH step on given inputs (tests only): per lane, the log-posterior
+// constants of bi:291-310 (x, z, T, tau, mean row (m0, m1), precision p00/p01/p11), the current
+// point (ll, lm), one proposal's t3 noise (t_l, t_m), the scales (s00, s11) and log U.  Runs the
+// same cust_coeffs (current log posterior, Q3 cap) and mh_step (fma + clip proposal, accept rule)
+// the sweep kernels inline.  out[lane] = {cur, plp, ll', lm', cur'} with plp = log_post_fast of
+// the clipped proposal (before the pm > 5 cap).
+__global__ void debug_mh_kernel(const int32_t* x, const uint8_t* z, const double* T, const double* tau,
+                                const double* m, const double* prec, const double* cur_pt, const float* t3,
+                                const double* scale, const float* log_u, int64_t n, double* out) {
+  __shared__ double tab[EXP_TAB_N];
+  for (int j = threadIdx.x; j < EXP_TAB_N; j += blockDim.x) tab[j] = EXP2_TAB[j];
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double H[HS];
+  for (int j = 0; j < HS; ++j) H[j] = 0.0;
+  H[H_BETA + 0] = m[2 * i];      // K = 1: X @ beta = 1 * beta = the given mean row, exactly
+  H[H_BETA + 1] = m[2 * i + 1];
+  H[H_P00] = prec[0];
+  H[H_P01] = prec[1];
+  H[H_P11] = prec[2];
+  Cust<2, 1> u;
+  u.xr[0] = 1.0;
+  u.xm = (double)x[i];
+  u.z = z[i] != 0;
+  u.lc.xm = u.xm;
+  u.lc.omz = u.z ? 0.0 : 1.0;  // as cust_ztau sets them (bi:299-301)
+  u.lc.w = u.z ? T[i] : tau[i];
+  u.ll = cur_pt[2 * i];
+  u.lm = cur_pt[2 * i + 1];
+  cust_coeffs<2, 1, false>(u, H, tab);
+  const double cur0 = u.cur;
+  const double pl = clip70_fma(scale[0], (double)t3[2 * i], u.ll);
+  const double pm = clip70_fma(scale[1], (double)t3[2 * i + 1], u.lm);
+  const double plp = log_post_fast(u.fc, pl, pm, tab);
+  mh_step(u, scale[0], scale[1], t3[2 * i], t3[2 * i + 1], log_u[i], tab);
+  double* o = out + 7 * i;
+  o[0] = cur0;
+  o[1] = plp;
+  o[2] = pl;
+  o[3] = pm;
+  o[4] = u.ll;
+  o[5] = u.lm;
+  o[6] = u.cur;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1980,6 +2030,14 @@ hipError_t launch_debug_hyper_variates(uint64_t seed, int chain, uint32_t sweep,
 
 hipError_t launch_debug_exp(const double* x, int64_t n, double* out, hipStream_t st) {
   hipLaunchKernelGGL(debug_exp_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, n, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_debug_mh(const int32_t* x, const uint8_t* z, const double* T, const double* tau, const double* m,
+                           const double* prec, const double* cur_pt, const float* t3, const double* scale,
+                           const float* log_u, int64_t n, double* out, hipStream_t st) {
+  hipLaunchKernelGGL(debug_mh_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, z, T, tau, m, prec,
+                     cur_pt, t3, scale, log_u, n, out);
   return hipGetLastError();
 }
 

@@ -234,8 +234,21 @@ class ShardedSampler:
     def step(self, n: int = 1) -> None:
         torch = self.torch
         if self.exchange == "p2p":  # one persistent launch per rank; every rank calls with the same n
-            self.s.run(n)
-            return
+            err = None
+            try:
+                self.s.run(n)
+            except _lib.ClvError as e:  # a wait timed out: this rank's state is unchanged
+                err = e
+            if self._all_ok(err is None):
+                return
+            # some rank's launch failed: every rank returns to the state before this step (ranks
+            # whose launch completed undo it) and the step is redone through the all-gather path
+            if err is None:
+                self.s.rollback()
+            self.exchange = "rccl"
+            self.p2p_note = (f"peer exchange failed at sweep {self.s.sweeps_done + 1} "
+                             f"({err or 'on another rank'}); continued on the all-gather path")
+            self.graph = None
         left = n
         if self.graph_chunk and not self.timing:
             if self.graph is None and left >= self.graph_chunk:

@@ -113,7 +113,12 @@ def make_prior(p: Problem, n_global: Optional[int] = None) -> _lib.ClvPrior:
 def resolve_seed(seed: Optional[int]) -> int:
     if seed is None:  # reference: default_rng(None) -> OS entropy (bi:486)
         return int(np.random.SeedSequence().entropy) & ((1 << 63) - 1)
-    return int(seed) & ((1 << 64) - 1)
+    seed = int(seed)
+    if seed < 0:  # numpy: default_rng(seed + ch) with a negative seed raises (bi:486)
+        raise ValueError("expected non-negative integer")
+    if seed >= 1 << 64:
+        raise ValueError("seed must fit 64 bits (the Philox key)")
+    return seed
 
 
 _SINKS = {"full": _lib.SINK_FULL, "summary": _lib.SINK_SUMMARY, "none": _lib.SINK_NONE}
@@ -189,6 +194,10 @@ class HipSampler:
     # ---- running
     def run(self, n_sweeps: int) -> None:
         check(self._L.clv_run(self.h, int(n_sweeps)))
+
+    def rollback(self) -> None:
+        """Undo the last completed persistent clv_run (clv_rollback)."""
+        check(self._L.clv_rollback(self.h))
 
     def sweep(self) -> None:
         check(self._L.clv_sweep(self.h))
@@ -334,19 +343,23 @@ class HipSampler:
 
 
 def run_with_trace(s: HipSampler, total: int, trace: int, n_chains_label: int = 1, chain_offset: int = 0) -> None:
-    """Run ``total`` sweeps, printing the reference's trace line (bi:384-385) for every chain at
-    every multiple of ``trace`` (chains advance together here, so lines come grouped by step)."""
+    """Run ``total`` sweeps, printing the reference's trace line (bi:383-384) for every chain at
+    every step that is a multiple of ``trace``, in the reference's order: its chains run one after
+    another (bi:484), so all lines of chain 1 come before any line of chain 2.  Here the chains
+    advance together: chain 1's lines are printed live (as the reference does, before the step
+    runs), the other chains' lines — identical text — once all sweeps are done."""
+    marks = [m for m in range(trace, total + 1, trace)] if trace else []
     done = 0
-    while done < total:
-        if trace:
-            nxt = min(total, (done // trace + 1) * trace)
-        else:
-            nxt = total
-        s.run(nxt - done)
-        done = nxt
-        if trace and done % trace == 0:
-            for ch in range(n_chains_label):
-                print(f"chain {chain_offset + ch + 1} | step {done}/{total}")
+    for m in marks:
+        if m - 1 > done:  # the reference prints at the start of step m
+            s.run(m - 1 - done)
+            done = m - 1
+        print(f"chain {chain_offset + 1} | step {m}/{total}")
+    if total > done:
+        s.run(total - done)
+    for ch in range(1, n_chains_label):
+        for m in marks:
+            print(f"chain {chain_offset + ch + 1} | step {m}/{total}")
 
 
 def fit(p: Problem, *, mcmc: int, burnin: int, thin: int, chains: int, seed, trace: int, n_mh_steps: int,

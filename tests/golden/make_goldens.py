@@ -12,6 +12,8 @@ Fixtures written:
   formulas.npz               G1: p_alive / tau / log_posterior / level-2 algebra from the reference
   replay_*.npz               G2: recorded variates + the reference's outputs for replay parity
   envelope_*.npz             G3: per-customer posterior summaries over M independent reference chains
+                             (abe subset: c1/bi K=2/tri K=3; full CDNOW: c2 and c3 at reduced length)
+  oracle_pin_full.json       the bitwise oracle-vs-reference checks on the full CDNOW c2/c3 inputs
   published_table3.json      abe_replication.xlsx "Table 3" (published loose pins)
   oracle_pin.json            the bitwise oracle-vs-reference checks that passed
   analysis_abe400.npz        row f: the reference's analysis helpers (draw_future_transactions bi/tri,
@@ -302,9 +304,10 @@ def write_replay(rbi, rtri):
 
 # ---------------------------------------------------------------------------------------------
 def _envelope_chain(args):
-    kind, covs, seed, burnin, mcmc = args
+    kind, covs, seed, burnin, mcmc = args[:5]
+    data = args[5] if len(args) > 5 else "abe"
     os.environ["OMP_NUM_THREADS"] = "1"
-    df = prepare(load_cbs("abe"))
+    df = prepare(load_cbs(data))
     fn = orc.mcmc_draw_parameters if kind == "bi" else orc.mcmc_draw_parameters_rfm_m
     d = fn(df, covs, mcmc=mcmc, burnin=burnin, thin=1, chains=1, seed=seed, trace=0)
     l1 = d["level_1"][0]
@@ -334,6 +337,41 @@ def write_envelope(M=16, burnin=2000, mcmc=2000):
         out["loglik"] = np.array([r[2] for r in rs])
         np.savez_compressed(os.path.join(HERE, f"envelope_{name}.npz"), **out)
         print("envelope", name)
+
+
+def write_envelope_full(rbi, rtri, M=16, burnin=1000, mcmc=1000):
+    """G3 at full size ("c2 and c3 at reduced length"): the full CDNOW CBS (23,570
+    customers) with c2's covariate (bivariate K=2) and c3's (trivariate K=3).  First re-pins the
+    oracle bitwise against the reference on these exact inputs (4 sweeps, 2 chains, every sweep
+    stored), then runs M independent oracle chains of burnin + mcmc sweeps."""
+    df = prepare(load_cbs("full"))
+    cases = [("full_bi_k2", "bi", ["first_sales_scaled"]), ("full_tri_k3", "tri", ["gender_F", "age_scaled"])]
+    pins = []
+    for name, kind, covs in cases:
+        kw = dict(mcmc=2, burnin=2, thin=1, chains=2, seed=7, trace=0)
+        fn_r = rbi.mcmc_draw_parameters if kind == "bi" else rtri.mcmc_draw_parameters_rfm_m
+        fn_o = orc.mcmc_draw_parameters if kind == "bi" else orc.mcmc_draw_parameters_rfm_m
+        assert bitwise_equal(fn_r(df, covs, **kw), fn_o(df, covs, **kw)), name
+        pins.append(dict(case=name, n=len(df), covariates=covs, **kw, bitwise=True))
+        print("pinned", name)
+    jobs = [(kind, covs, 3000 + m, burnin, mcmc, "full") for _, kind, covs in cases for m in range(M)]
+    with Pool(min(8, len(jobs))) as pool:  # 1 thread per process
+        res = pool.map(_envelope_chain, jobs, chunksize=1)
+    for ci, (name, kind, covs) in enumerate(cases):
+        rs = res[ci * M:(ci + 1) * M]
+        out = dict(kind=kind, covariates=np.array(covs, dtype="U32"), M=M, burnin=burnin, mcmc=mcmc,
+                   data=np.array("full"), seeds=np.array([3000 + m for m in range(M)]))
+        for k in rs[0][0].keys():
+            v = np.stack([r[0][k] for r in rs])
+            out[k + "_mean"] = v.mean(0)
+            out[k + "_sd"] = v.std(0, ddof=1)
+            out[k + "_chains"] = v.mean(1)
+        out["level2_median"] = np.stack([r[1] for r in rs])
+        out["loglik"] = np.array([r[2] for r in rs])
+        np.savez_compressed(os.path.join(HERE, f"envelope_{name}.npz"), **out)
+        print("envelope", name)
+    with open(os.path.join(HERE, "oracle_pin_full.json"), "w") as f:
+        json.dump(dict(reference=REF, checks=pins), f, indent=1)
 
 
 # ---------------------------------------------------------------------------------------------
@@ -474,6 +512,7 @@ def main():
              ("dataprep", lambda: write_dataprep(rbi))]
     if not a.skip_envelope:
         steps.append(("envelope", write_envelope))
+        steps.append(("envelope_full", lambda: write_envelope_full(rbi, rtri)))
     for name, fn in steps:
         if only is None or name in only:
             fn()

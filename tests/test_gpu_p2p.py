@@ -167,3 +167,92 @@ def test_p2p_two_processes_ipc(D):
         import json
         res = json.loads(out.strip().splitlines()[-1])
         assert res["ok"], res
+
+
+def test_p2p_abort_leaves_state_unchanged_and_rollback(monkeypatch):
+    """a persistent launch whose wait times out (here: the peer rank never launches)
+    fails and leaves its rank's state, sweep count and summary sums exactly as before the call;
+    after reconnecting, and after a completed step is undone with clv_rollback on every rank and
+    redone, the run is still bitwise the unsharded one."""
+    import torch
+    from mcmc_clv_model_amd import _lib
+    from mcmc_clv_model_amd import distributed as Dm
+    from mcmc_clv_model_amd.sampler import HipSampler, build_problem, make_prior
+    monkeypatch.setenv("CLV_WAIT_TIMEOUT_MS", "300")
+    p = build_problem(cdnow("full", 23570), ["first_sales_scaled"], 2)
+    kw = dict(mcmc=9, burnin=1, thin=1, chains=2, seed=77, draw_sink="summary")
+    world = 2
+    ref, ref_sums, _, ref_l2, ref_ll = _ref_run(p, 10, kw)
+    plan = Dm.plan(p.N, world)
+    prior = make_prior(p, p.N)
+    shards = []
+    for r in range(world):
+        b, e = plan.shard(r)
+        shards.append(HipSampler(Dm.slice_problem(p, b, e), n_global=p.N, shard_begin=r * plan.blocks_per_rank * 256,
+                                 world_size=world, rank=r, blocks_per_rank=plan.blocks_per_rank,
+                                 blocks_per_unit=plan.blocks_per_unit, prior=prior, **kw))
+
+    def run_all(n, ranks=None):
+        errs = []
+
+        def go(sh):
+            try:
+                sh.run(n)
+            except Exception as e:  # noqa: BLE001
+                errs.append(e)
+        th = [threading.Thread(target=go, args=(shards[r],)) for r in (ranks or range(world))]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=60)
+        assert not any(t.is_alive() for t in th)
+        return errs
+
+    def connect():
+        ptrs = [sh.p2p_info()["mail_ptr"] for sh in shards]
+        for sh in shards:
+            sh.p2p_connect(ptrs=ptrs)
+        for sh in shards:
+            sh.synchronize()
+
+    try:
+        nd = shards[0].partials()[1]
+        gathered = torch.zeros(nd * world, dtype=torch.float64, device="cuda")
+        for r, sh in enumerate(shards):
+            sh.copy_partials(gathered.data_ptr() + r * nd * 8)
+            sh.synchronize()
+        for sh in shards:
+            sh.hyper(gathered.data_ptr())
+            sh.synchronize()
+        connect()
+        assert not run_all(3)
+        before = shards[0].get_state()
+        sums_before = shards[0].read_summary()[0].copy()
+        errs = run_all(4, ranks=[0])  # rank 1 never launches: rank 0's first wait times out
+        assert len(errs) == 1 and isinstance(errs[0], _lib.ClvError) and "state unchanged" in str(errs[0])
+        assert shards[0].sweeps_done == 3
+        after = shards[0].get_state()
+        assert all(np.array_equal(bits(x), bits(y)) for x, y in zip(before, after))
+        assert np.array_equal(bits(shards[0].read_summary()[0]), bits(sums_before))
+        assert not shards[0].p2p_info()["connected"]
+        connect()
+        assert not run_all(4)
+        assert not run_all(2)
+        for sh in shards:  # a completed step undone on every rank, then redone
+            sh.rollback()
+            assert sh.sweeps_done == 7
+        with pytest.raises(_lib.ClvError, match="nothing to roll back"):
+            shards[0].rollback()
+        assert not run_all(3)
+        for r, sh in enumerate(shards):
+            b, e = plan.shard(r)
+            assert sh.sweeps_done == 10
+            lam, mu, beta, sigma = sh.get_state()
+            assert np.array_equal(bits(lam), bits(ref[0][:, b:e])) and np.array_equal(bits(mu), bits(ref[1][:, b:e]))
+            assert np.array_equal(bits(beta), bits(ref[2])) and np.array_equal(bits(sigma), bits(ref[3]))
+            assert np.array_equal(bits(sh.read_summary()[0]), bits(ref_sums[:, :, b:e]))
+            _, l2, ll = sh.read_draws(level1=False)
+            assert np.array_equal(bits(l2), bits(ref_l2)) and np.array_equal(bits(ll), bits(ref_ll))
+    finally:
+        for sh in shards:
+            sh.close()

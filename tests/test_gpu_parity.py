@@ -261,7 +261,8 @@ def test_trace_lines(L, capsys):
     df = cdnow("abe", 100)
     _bi(df, mcmc=4, burnin=4, thin=1, chains=2, trace=4)
     out = capsys.readouterr().out.splitlines()
-    assert out == ["chain 1 | step 4/8", "chain 2 | step 4/8", "chain 1 | step 8/8", "chain 2 | step 8/8"]
+    # the reference's order: its chains run one after another (bi:383-384, bi:484)
+    assert out == ["chain 1 | step 4/8", "chain 1 | step 8/8", "chain 2 | step 4/8", "chain 2 | step 8/8"]
 
 
 @pytest.mark.parametrize("D,covs,n", [(2, ["first_sales_scaled"], 23570), (3, ["gender_F", "age_scaled"], 2357),
@@ -482,3 +483,98 @@ def test_persistent_kernel_bitwise_equals_launch_per_sweep(L, D, covs, n, sink, 
     for x, y in zip(a[2:], b[2:]):
         if x is not None:
             assert np.array_equal(bits(x), bits(y))
+
+
+def _mh_step_device(L, f, t3, log_u, cur_pt=None):
+    """clv_debug_mh_step over formulas.npz's log-posterior inputs (G1, bi:291-310)."""
+    n = f["lp_ll"].size
+    S = f["lp_S"]
+    P = np.linalg.inv(S)
+    x = np.ascontiguousarray(f["lp_x"], dtype=np.int32)
+    z = np.ascontiguousarray(f["lp_z"], dtype=np.uint8)
+    T = np.ascontiguousarray(f["lp_T"], dtype=np.float64)
+    tau = np.ascontiguousarray(f["lp_tau"], dtype=np.float64)
+    m = np.ascontiguousarray(f["lp_mv"], dtype=np.float64)
+    prec = np.array([P[0, 0], P[0, 1], P[1, 1]])
+    cur = np.ascontiguousarray(np.column_stack([f["lp_ll"], f["lp_lm"]]) if cur_pt is None else cur_pt)
+    scale = np.array([S[0, 0], S[1, 1]])
+    out = np.zeros((n, 7))
+    rc = L.clv_debug_mh_step(n, x.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                             z.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), _dp(T), _dp(tau), _dp(m), _dp(prec),
+                             _dp(cur), _fp(np.ascontiguousarray(t3, dtype=np.float32)), _dp(scale),
+                             _fp(np.ascontiguousarray(log_u, dtype=np.float32)), _dp(out))
+    assert rc == 0
+    return out
+
+
+def test_device_mh_step_matches_reference_log_posterior(L):
+    """The SHIPPED Philox-mode MH step (log_post_fast, fma + clip proposal, accept iff pm <= 5 and
+    plp > cur + log U) on formulas.npz's log-posterior inputs, which include the reference's edge
+    cases: lm > 5 -> lp = -inf (quirk Q3, bi:309) and -inf - -inf = NaN (never accepted, bi:329-330).
+    Checked against the reference's log posterior (the oracle, bitwise = bi:291-310):
+      * lp differences plp - cur equal the reference's within 1e-12 of the terms' magnitude;
+      * current points with lm > 5 have cur = -inf; proposals with pm > 5 are never accepted;
+      * accept decisions equal the reference's exp(lp' - lp) > U (U = exp(log U)) wherever the
+        margin |lp' - lp - log U| exceeds the arithmetic tolerance (about half the lanes are placed
+        close to their margin on purpose);
+      * every accepted lane carries exactly (pl, pm, plp), every rejected lane exactly its input;
+      * a padded step (log U = +inf) never accepts, also from a cur = -inf point."""
+    from oracle import ref_cpu as orc
+    f = golden("formulas.npz")
+    n = f["lp_ll"].size
+    rng = np.random.default_rng(2024)
+    t3 = rng.standard_t(3, (n, 2)).astype(np.float32)
+    P = np.linalg.inv(f["lp_S"])
+    args = (f["lp_x"], f["lp_z"], f["lp_T"], f["lp_tau"], f["lp_mv"], P)
+    # first pass only to get the device's proposals; log U chosen after from the reference's deltas
+    out0 = _mh_step_device(L, f, t3, np.full(n, np.inf, np.float32))
+    pl, pm = out0[:, 2], out0[:, 3]
+    assert np.array_equal(out0[:, 4], f["lp_ll"]) and np.array_equal(out0[:, 5], f["lp_lm"])  # +inf: no accept
+    ref_pl = np.clip(f["lp_ll"] + f["lp_S"][0, 0] * t3[:, 0].astype(np.float64), -70.0, 70.0)
+    np.testing.assert_allclose(pl, ref_pl, rtol=1e-15, atol=1e-13)  # fma vs two roundings
+    with np.errstate(over="ignore", invalid="ignore"):
+        lp_cur = orc.log_posterior(f["lp_ll"], f["lp_lm"], *args)
+        lp_prop = orc.log_posterior(pl, pm, *args)
+        d_ref = lp_prop - lp_cur
+    assert np.array_equal(bits(lp_cur), bits(f["lp_out"]))  # the oracle is the reference here
+    # log U: half the lanes near the margin (d_ref + small offset), half uniform log U
+    lu = np.log(rng.random(n)).astype(np.float32)
+    near = (rng.random(n) < 0.5) & np.isfinite(d_ref) & (np.abs(d_ref) < 50)
+    lu[near] = (np.minimum(d_ref[near], 0.0) + rng.choice([-1, 1], near.sum()) * 10.0 ** rng.uniform(-6, -1, near.sum())
+                ).astype(np.float32)
+    lu = np.minimum(lu, np.float32(-1e-30))  # log U < 0 (U < 1)
+    out = _mh_step_device(L, f, t3, lu)
+    cur, plp = out[:, 0], out[:, 1]
+    # Q3 on the current point
+    assert np.all(np.isneginf(cur[f["lp_lm"] > 5.0])) and np.all(np.isfinite(cur[f["lp_lm"] <= 5.0]))
+    # lp differences
+    ll, lm = f["lp_ll"], f["lp_lm"]
+    w = np.where(f["lp_z"], f["lp_T"], f["lp_tau"])
+    mv = f["lp_mv"]
+    quad = lambda a, b: (np.abs(a - mv[:, 0]) + np.abs(b - mv[:, 1])) ** 2 * np.abs(P).max()  # noqa: E731
+    mag = (np.abs(f["lp_x"] * ll) + np.abs(f["lp_x"] * pl) + np.abs(lm) + np.abs(pm)
+           + w * (np.exp(np.minimum(ll, 700)) + np.exp(np.minimum(lm, 700)) + np.exp(pl) + np.exp(pm))
+           + quad(ll, lm) + quad(pl, pm) + np.abs(mv).sum(1) ** 2 * np.abs(P).max() + 1.0)
+    fin = (lm <= 5.0) & (pm <= 5.0)
+    d_dev = plp - cur
+    err = np.abs(d_dev[fin] - d_ref[fin])
+    assert np.all(err <= 1e-12 * mag[fin]), (err / mag[fin]).max()
+    # accept decisions
+    with np.errstate(over="ignore", invalid="ignore"):
+        acc_ref = np.exp(d_ref) > np.exp(lu.astype(np.float64))
+    acc_dev = (out[:, 4] == pl) & (out[:, 5] == pm) & (out[:, 6] == plp)
+    rej_dev = (out[:, 4] == ll) & (out[:, 5] == lm) & (bits(out[:, 6]) == bits(cur))
+    assert np.all(acc_dev | rej_dev)
+    margin = np.abs(d_ref - lu.astype(np.float64))
+    clear = ~(np.isfinite(margin) & (margin <= 1e-12 * mag))
+    assert clear.sum() > 0.95 * n
+    assert np.array_equal(acc_dev[clear & ~(acc_dev & rej_dev)], acc_ref[clear & ~(acc_dev & rej_dev)])
+    assert not np.any(acc_dev & (pm > 5.0) & ~rej_dev)                 # capped proposals never taken
+    both_inf = (lm > 5.0) & (pm > 5.0)                                # reference: NaN ratio -> reject
+    assert both_inf.sum() > 0 and not np.any(acc_ref[both_inf]) and np.all(rej_dev[both_inf])
+    from_inf = (lm > 5.0) & (pm <= 5.0)                               # reference: +inf ratio -> accept
+    assert from_inf.sum() > 0 and np.all(acc_ref[from_inf]) and np.all(acc_dev[from_inf])
+    assert 0.05 * n < acc_dev.sum() < 0.95 * n
+    # padded steps from cur = -inf points: thr = -inf + inf = NaN, never accepted
+    out2 = _mh_step_device(L, f, t3, np.full(n, np.inf, np.float32))
+    assert np.array_equal(out2[:, 4], ll) and np.array_equal(out2[:, 5], lm)

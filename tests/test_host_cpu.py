@@ -188,7 +188,7 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("n_global", [23570, 140_000])
+@pytest.mark.parametrize("n_global", [23570, 140_000, 1_000_000])  # c2, a mid size, c4 (1M, strong scaling)
 def test_sharded_exchange_world2_gloo_matches_single_process(n_global):
     import multiprocessing as mp
     from mcmc_clv_model_amd import distributed as D
@@ -266,3 +266,25 @@ def test_persistent_placement_map(C, nb, n_cu):
     assert all(i < P or i >= n_cu for i in l2)  # every level-2 workgroup sits on a shared CU
     pairs = np.bincount(chain[:P], minlength=C)
     assert pairs.max() - pairs.min() <= 1  # shared CUs spread evenly over the chains
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_bench_scaling_workloads(world, monkeypatch):
+    """bench.py's BASELINE multi-GPU configurations: c4 keeps the same problem at
+    every N (strong scaling), c5 grows by its per-GPU size (weak scaling), with the covariate
+    counts K = 5 / 9; the shard plan covers every customer.  Sizes scaled down 1000x here."""
+    import bench
+    from mcmc_clv_model_amd import distributed as D
+    monkeypatch.setitem(bench.WORKLOADS, "c4", bench.WORKLOADS["c4"][:1] + ("synthetic:1000:5:20250718",)
+                        + bench.WORKLOADS["c4"][2:])
+    monkeypatch.setitem(bench.WORKLOADS, "c5", bench.WORKLOADS["c5"][:1] + ("synthetic:1250:9:20250719",)
+                        + bench.WORKLOADS["c5"][2:])
+    df4, D4, covs4 = bench.load_workload("c4", world)[:3]
+    df5, D5, covs5 = bench.load_workload("c5", world)[:3]
+    assert (len(df4), D4, len(covs4) + 1) == (1000, 2, 5)
+    assert (len(df5), D5, len(covs5) + 1) == (1250 * world, 3, 9)
+    assert set(covs5) <= set(df5.columns) and "log_s" in df5.columns
+    for n in (len(df4), len(df5)):
+        pl = D.plan(n, world)
+        spans = [pl.shard(r) for r in range(world)]
+        assert spans[0][0] == 0 and spans[-1][1] == n

@@ -6,6 +6,7 @@ the fraction of customers within 4 sigma and the mean per-customer z.  What the 
 against itself is the bar the GPU sampler's ensembles can be held to.
 
 Usage: python tools/envelope_ref_calibration.py c1_bi_k1 2000,3000 [M]
+       python tools/envelope_ref_calibration.py full_bi_k2 5000 [M]   (c2 at 1000 + 1000 sweeps)
 """
 import os
 import sys
@@ -25,7 +26,8 @@ def _chain(args):
     f = golden(f"envelope_{name}.npz")
     covs = [str(c) for c in f["covariates"]]
     fn = orc.mcmc_draw_parameters if str(f["kind"]) == "bi" else orc.mcmc_draw_parameters_rfm_m
-    d = fn(cdnow("abe"), covs, mcmc=int(f["mcmc"]), burnin=int(f["burnin"]), thin=1, chains=1, seed=seed, trace=0)
+    data = str(f["data"]) if "data" in f.files else "abe"
+    d = fn(cdnow(data), covs, mcmc=int(f["mcmc"]), burnin=int(f["burnin"]), thin=1, chains=1, seed=seed, trace=0)
     l1 = d["level_1"][0]
     st = dict(log_lambda=np.log(l1[:, :, 0]).mean(0), log_mu=np.log(l1[:, :, 1]).mean(0),
               p_alive=l1[:, :, 3].mean(0), lam=l1[:, :, 0].mean(0))
