@@ -17,6 +17,28 @@
 #include "kernels.h"
 #include "philox.h"
 
+#ifndef SWEEP_MH_PIPELINE
+#define SWEEP_MH_PIPELINE 1  // 1: next MH chunk's variates drawn during the current chunk's steps
+#endif
+#ifndef PERSIST_REDUCE_GEN
+#define PERSIST_REDUCE_GEN 1  // persistent kernel: statistics formed chunk-wise in the reduction
+#endif
+#ifndef SWEEP_REDUCE_CHUNK
+#define SWEEP_REDUCE_CHUNK 8  // statistics formed and reduced per chunk in the customer workgroups
+#endif
+// sweep_kernel __launch_bounds__ minimum workgroups per CU: 4 (<= 128 VGPRs, 4 waves per SIMD) for
+// the bivariate instances up to K = 5 — c4 (1M, K=5) 104.4 -> 101.0 us per sweep — and the
+// compiler's choice (168 VGPRs, 3 waves) for the trivariate ones, where the 128-register cap
+// spills (c5 151 -> 160 us).  SWEEP_MIN_BLOCKS overrides (A/B builds).
+template <int D, int K>
+struct SweepOcc {  // waves per SIMD the launched instance is compiled for (sweep_kernel_occ4 if 4)
+#ifdef SWEEP_MIN_BLOCKS
+  static constexpr int value = SWEEP_MIN_BLOCKS;  // 4: every instance occ4, else none
+#else
+  static constexpr int value = (D == 2 && K <= 5) ? 4 : 1;
+#endif
+};
+
 namespace clv {
 
 
@@ -154,6 +176,94 @@ __device__ __forceinline__ void block_reduce(double (&v)[NS], double (*red)[NS],
   }
   if constexpr (LDS_ONLY) lds_barrier(); else __syncthreads();
 }
+
+// The same reduction with the NS values produced on demand, G at a time (gen(j) = element j), so
+// at most G of them are live in registers: every element is summed over the lanes in exactly the
+// order of block_reduce (lane l + lane l+32, then row pairs, then the DPP rotate), whatever its
+// partner in the swaps — results are bitwise those of block_reduce on the materialised array.
+template <int NS, int G, int NT = BLOCK, class Gen>
+__device__ __forceinline__ void block_reduce_gen(const Gen& gen, double (*red)[NS], double* out) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  constexpr int NW = NT / 64;
+#pragma unroll
+  for (int base = 0; base < NS; base += G) {
+    constexpr int GG = G;
+    const int n = NS - base < GG ? NS - base : GG;  // compile-time after unrolling
+    const int h1 = (n + 1) / 2;
+    const int h2 = (h1 + 1) / 2;
+    double w1[(G + 1) / 2];
+#pragma unroll
+    for (int j = 0; j < (G + 1) / 2; ++j) {
+      if (j < h1) {
+        double a = gen(base + j);
+        double b = (j + h1 < n) ? gen(base + j + h1) : 0.0;
+        swap_halves(a, b);
+        w1[j] = a + b;
+      }
+    }
+    double w2[(G + 3) / 4];
+#pragma unroll
+    for (int j = 0; j < (G + 3) / 4; ++j) {
+      if (j < h2) {
+        double a = w1[j];
+        double b = (j + h2 < h1) ? w1[j + h2] : 0.0;
+        swap_rows(a, b);
+        double x = a + b;
+        x = add_row_ror<8>(x);
+        x = add_row_ror<4>(x);
+        x = add_row_ror<2>(x);
+        x = add_row_ror<1>(x);
+        w2[j] = x;
+      }
+    }
+    if ((lane & 15) == 0) {
+      const int row = lane >> 4;
+#pragma unroll
+      for (int j = 0; j < (G + 3) / 4; ++j) {
+        const int i1 = j + ((row & 1) ? h2 : 0);
+        const int idx = i1 + ((row >> 1) ? h1 : 0);
+        if (j < h2 && i1 < h1 && idx < n) red[wave][base + idx] = w2[j];
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < NS) {
+    double t = red[0][threadIdx.x];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) t += red[w][threadIdx.x];
+    out[threadIdx.x] = t;
+  }
+  __syncthreads();
+}
+
+// One customer's level-2 sufficient statistics as a generator (element j of X'Y (K x D), the
+// upper triangle of Y'Y, the likelihood term), each 0.0 + value as the accumulation from zero
+// gave it, and 0.0 for an inactive lane.
+template <int D, int K>
+struct StatGen {
+  double xr[K];  // by value (constant indices after unrolling: registers, no private-memory array)
+  double Y[D];
+  double lik;
+  bool on;
+  __device__ __forceinline__ double operator()(int j) const {
+    double v;
+    if (j < K * D) {
+      v = xr[j / D] * Y[j % D];
+    } else if (j < K * D + D * (D + 1) / 2) {
+      v = 0.0;
+      int t = K * D;
+#pragma unroll
+      for (int p = 0; p < D; ++p)
+#pragma unroll
+        for (int q = p; q < D; ++q, ++t)
+          if (t == j) v = Y[p] * Y[q];
+    } else {
+      v = lik;
+    }
+    return on ? 0.0 + v : 0.0;
+  }
+};
 
 // bi:402 (the reference's loop ends at burnin + mcmc, bi:383, so nothing beyond is stored)
 #ifdef CLV_STAMPS
@@ -958,6 +1068,16 @@ __device__ __forceinline__ void mh_run(Cust<D, K>& cu, const SlotPhilox& ph, dou
   const int n_chunks = (S + MC - 1) / MC;
   if (n_chunks <= 0) return;
   float tl[MC], tm[MC], lu[MC];
+#if SWEEP_MH_PIPELINE == 0
+  // no software pipeline (occupancy hides the latency instead): variates, then the chunk's steps
+  for (int ch = 0; ch < n_chunks; ++ch) {
+    mh_chunk_variates(ph, (uint32_t)ch, tl, tm, lu);
+    const int rem = S - ch * MC;
+#pragma unroll
+    for (int st = 0; st < MC; ++st) mh_step(cu, s00, s11, tl[st], tm[st], st < rem ? lu[st] : __builtin_inff(), exp_tab);
+  }
+  return;
+#endif
   mh_chunk_variates(ph, 0u, tl, tm, lu);
   for (int ch = 0; ch + 1 < n_chunks; ++ch) {
     float ntl[MC], ntm[MC], nlu[MC];
@@ -979,27 +1099,29 @@ __device__ __forceinline__ void mh_run(Cust<D, K>& cu, const SlotPhilox& ph, dou
 // Persistent kernel: the MH variates of a whole sweep (up to PRE_STEPS steps) drawn ahead, while
 // the wave would otherwise idle in the level-2 hand-off; the MH phase after (beta, Sigma) arrive is
 // then only the dependent fp64 accept/reject chain.  Steps >= S carry log U = +inf (never taken).
+// The variates live in LDS, one column per lane (each lane reads back only what it wrote: no
+// barrier), not in 60 VGPRs: the persistent kernel's customer path spilled with them in registers.
 constexpr int PRE_STEPS = 20;
+constexpr int PRE_LDS_BYTES = PRE_STEPS * BLOCK * 12;  // float2 (t_l, t_m) + float log U per step and lane
 struct PreVariates {
-  float tl[PRE_STEPS], tm[PRE_STEPS], lu[PRE_STEPS];
+  float2* t;  // [PRE_STEPS][BLOCK]
+  float* u;   // [PRE_STEPS][BLOCK]
+  int lane;
 };
 
-__device__ __forceinline__ void mh_pre_variates(const SlotPhilox& ph, int S, PreVariates& v) {
+__device__ __forceinline__ void mh_pre_variates(const SlotPhilox& ph, int S, const PreVariates& v) {
   constexpr int MC = MH_CHUNK_STEPS;
 #pragma unroll
   for (int q = 0; q < PRE_STEPS / MC; ++q) {
-    float tl[MC], tm[MC], lu[MC];
     if (q * MC < S) {  // wave-uniform
+      float tl[MC], tm[MC], lu[MC];
       mh_chunk_variates(ph, (uint32_t)q, tl, tm, lu);
-    } else {
 #pragma unroll
-      for (int st = 0; st < MC; ++st) tl[st] = tm[st] = 0.0f;
-    }
-#pragma unroll
-    for (int st = 0; st < MC; ++st) {
-      v.tl[q * MC + st] = tl[st];
-      v.tm[q * MC + st] = tm[st];
-      v.lu[q * MC + st] = q * MC + st < S ? lu[st] : __builtin_inff();
+      for (int st = 0; st < MC; ++st) {
+        const int k = q * MC + st;
+        v.t[k * BLOCK + v.lane] = make_float2(tl[st], tm[st]);
+        v.u[k * BLOCK + v.lane] = k < S ? lu[st] : __builtin_inff();
+      }
     }
   }
 }
@@ -1011,9 +1133,15 @@ __device__ __forceinline__ void mh_run_pre(Cust<D, K>& cu, const PreVariates& v,
 #pragma unroll
   for (int q = 0; q < PRE_STEPS / MC; ++q) {
     if (q * MC < S) {  // wave-uniform
+      float2 t[MC];
+      float u[MC];
 #pragma unroll
-      for (int st = 0; st < MC; ++st)
-        mh_step(cu, s00, s11, v.tl[q * MC + st], v.tm[q * MC + st], v.lu[q * MC + st], exp_tab);
+      for (int st = 0; st < MC; ++st) {  // the chunk's LDS reads issued together, ahead of the chain
+        t[st] = v.t[(q * MC + st) * BLOCK + v.lane];
+        u[st] = v.u[(q * MC + st) * BLOCK + v.lane];
+      }
+#pragma unroll
+      for (int st = 0; st < MC; ++st) mh_step(cu, s00, s11, t[st].x, t[st].y, u[st], exp_tab);
     }
   }
 }
@@ -1025,11 +1153,10 @@ struct CustOut {
   double lam, mu, eta, lgl, lgm;
 };
 
-template <int D, int K, bool REPLAY, int NS>
+template <int D, int K, bool REPLAY>
 __device__ __forceinline__ CustOut<D> cust_finish(Cust<D, K>& u, const SweepArgs& a, int64_t s, bool stored,
                                                   const double* H, uint32_t k0, uint32_t k1, const double* tape,
-                                                  const double* exp_tab, double (&acc)[NS]) {
-  constexpr int NXY = K * D;
+                                                  const double* exp_tab, StatGen<D, K>& st) {
   const Geometry& g = a.g;
   const int64_t i = u.i;
   // bi:337-338 (state back to natural scale).  Replay reproduces the reference's exp/log round
@@ -1078,17 +1205,14 @@ __device__ __forceinline__ CustOut<D> cust_finish(Cust<D, K>& u, const SweepArgs
   }
   u.lam = lam;
   u.mu = mu;
-  // ---- sufficient statistics: X'Y (K x D), Y'Y (upper triangle), likelihood term
+  // ---- sufficient statistics X'Y (K x D), Y'Y (upper triangle), likelihood term: formed in the
+  // workgroup reduction (block_reduce_gen), a few at a time
 #pragma unroll
-  for (int k = 0; k < K; ++k)
+  for (int k = 0; k < K; ++k) st.xr[k] = u.xr[k];
 #pragma unroll
-    for (int d = 0; d < D; ++d) acc[k * D + d] += u.xr[k] * Y[d];
-  int t = NXY;
-#pragma unroll
-  for (int p = 0; p < D; ++p)
-#pragma unroll
-    for (int q = p; q < D; ++q) acc[t++] += Y[p] * Y[q];
-  acc[NS - 1] += lik;
+  for (int d = 0; d < D; ++d) st.Y[d] = Y[d];
+  st.lik = lik;
+  st.on = true;
   return CustOut<D>{lam, mu, eta, lgl, lgm};
 }
 
@@ -1134,7 +1258,7 @@ __device__ __forceinline__ void cust_store(const Cust<D, K>& u, const CustOut<D>
 static_assert(BLOCK == EXP_TAB_N, "the sweep kernel stages the exp table with one entry per lane");
 
 template <int D, int K, bool REPLAY>
-__global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
+__device__ __forceinline__ void sweep_body(const SweepArgs& a) {
   constexpr int NT = BLOCK;
   constexpr int NXY = K * D;
   constexpr int NYY = D * (D + 1) / 2;
@@ -1164,9 +1288,7 @@ __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
   const int64_t s = a.init ? 0 : a.ctrl->cur + 1;
   const bool stored = !a.init && is_stored(s, g);
 
-  double acc[NS];
-#pragma unroll
-  for (int j = 0; j < NS; ++j) acc[j] = 0.0;
+  StatGen<D, K> st{};
   if (threadIdx.x == 0 && !a.init) {
     CLV_STAMP(a.stamps, s, 0, true);
     CLV_STAMP(a.stamps, s, 5, false);
@@ -1183,25 +1305,16 @@ __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
       const double tx = a.tx[i];
       const double lam = a.lam_init;
       const double mu = 1.0 / (tx + 0.5 / a.lam_init);
-      double xr[K], Y[D];
-      xr[0] = 1.0;
+      st.xr[0] = 1.0;
 #pragma unroll
-      for (int k = 1; k < K; ++k) xr[k] = a.cov[(int64_t)(k - 1) * g.n + i];
-      Y[0] = log(lam);
-      Y[1] = log(mu);
-      if constexpr (D == 3) Y[2] = 0.0;
+      for (int k = 1; k < K; ++k) st.xr[k] = a.cov[(int64_t)(k - 1) * g.n + i];
+      st.Y[0] = log(lam);
+      st.Y[1] = log(mu);
+      if constexpr (D == 3) st.Y[2] = 0.0;
+      st.on = true;
       const int64_t ci = (int64_t)c * g.n + i;
       a.lam[ci] = lam;
       a.mu[ci] = mu;
-#pragma unroll
-      for (int k = 0; k < K; ++k)
-#pragma unroll
-        for (int d = 0; d < D; ++d) acc[k * D + d] += xr[k] * Y[d];
-      int t = NXY;
-#pragma unroll
-      for (int p = 0; p < D; ++p)
-#pragma unroll
-        for (int r = p; r < D; ++r) acc[t++] += Y[p] * Y[r];
     }
   }
   if (!REPLAY) exp_tab[threadIdx.x] = tab_v;
@@ -1272,10 +1385,10 @@ __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
       mh_run(cu, SlotPhilox(k0, k1, cu.gi, (uint32_t)s), s00, s11, g.S, exp_tab);
     }
     if (threadIdx.x == 0) CLV_WG_STAMP(a.stamps, (int64_t)c * g.nb_local + b, 6);
-    out = cust_finish<D, K, REPLAY, NS>(cu, a, s, stored, H, k0, k1, tape, exp_tab, acc);
+    out = cust_finish<D, K, REPLAY>(cu, a, s, stored, H, k0, k1, tape, exp_tab, st);
   }
 
-  block_reduce<NS>(acc, red, tot);
+  block_reduce_gen<NS, SWEEP_REDUCE_CHUNK>(st, red, tot);
   if (threadIdx.x < NS)  // sc1 (write-through) store: read cross-CU by the fused tail
     __hip_atomic_store(a.blockpart + ((int64_t)c * g.stride + threadIdx.x) * g.blocks_per_rank + b, tot[threadIdx.x],
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1351,6 +1464,18 @@ __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
   }
 }
 
+
+// The sweep kernel at two occupancy targets (an attribute cannot depend on template arguments
+// here): see SweepOcc.
+template <int D, int K, bool REPLAY>
+__global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
+  sweep_body<D, K, REPLAY>(a);
+}
+template <int D, int K, bool REPLAY>
+__global__ __launch_bounds__(BLOCK, 4) void sweep_kernel_occ4(SweepArgs a) {
+  sweep_body<D, K, REPLAY>(a);
+}
+
 // ---------------------------------------------------------------------------------------------
 // Persistent sweep kernel (world size 1, Philox mode): one launch runs n_sweeps sweeps.  Grid
 // (nb_local + 1, chains), every workgroup resident at once (checked at create).  Per chain,
@@ -1408,7 +1533,7 @@ __device__ __forceinline__ bool wait_expired(const SweepArgs& a, uint64_t t0, ui
 // register arrays (block/unit partials of the chain) do not raise the customer path's pressure.
 template <int D, int K, bool P2P>
 __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_first, int64_t n_sweeps, int c, uint32_t k0,
-                                            uint32_t k1, int64_t wgi, int64_t it_stamp) {
+                                            uint32_t k1, int64_t wgi, int64_t it_stamp, double* pool) {
   constexpr int NT = BLOCK;
   constexpr int NXY = K * D;
   constexpr int NYY = D * (D + 1) / 2;
@@ -1516,7 +1641,8 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
         if (b1 < g.nb_local) acc[j] += v1[j];
       }
     } else {
-      __shared__ double umail[UMAIL];  // this rank's unit partials [stat][local unit]
+      double* umail = pool;  // [UMAIL]: this rank's unit partials [stat][local unit] (the pool the
+                             // customer workgroups use for their drawn-ahead MH variates)
       // 3a. this rank's unit partials: blocks_per_unit consecutive blocks summed in group_kernel's
       //     order (a unit's blocks sit in consecutive lanes of one wavefront: bpu | 64); with one
       //     block per unit the unit partial IS the block partial (the sharded path has no group
@@ -1676,6 +1802,9 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
   __shared__ double exp_tab[EXP_TAB_N];
   __shared__ double Hs[HS];
   __shared__ uint32_t s_abort;
+  // customer workgroups: the drawn-ahead MH variates; the level-2 workgroup (P2P): its unit partials
+  __shared__ __attribute__((aligned(16))) char pool[PRE_LDS_BYTES];
+  static_assert(UMAIL * sizeof(double) <= PRE_LDS_BYTES, "the level-2 unit partials share the variates' LDS");
   const Geometry& g = a.g;
   int c = blockIdx.y, b = blockIdx.x;
   if (a.wg_map) {  // placement (capi.hip persist_wg_map): same-chain workgroups share CUs
@@ -1694,7 +1823,7 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
   if (tid == 0) s_abort = 0;
 
   if (b == g.nb_local) {  // the chain's level-2 workgroup
-    persist_level2<D, K, P2P>(a, s_first, n_sweeps, c, k0, k1, wgi, it_stamp);
+    persist_level2<D, K, P2P>(a, s_first, n_sweeps, c, k0, k1, wgi, it_stamp, (double*)pool);
     return;
   }
 
@@ -1712,7 +1841,7 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
   if (cu.active) cust_ztau<D, K, false>(cu, a, s_first, k0, k1, nullptr, exp_tab);
   // MH variates drawn ahead (while the wave waits for the level-2 draw) when S fits the registers
   const bool pre = a.pre_variates && g.S <= PRE_STEPS;
-  PreVariates pv;
+  const PreVariates pv{(float2*)pool, (float*)(pool + PRE_STEPS * BLOCK * 8), tid};
   if (cu.active && pre) mh_pre_variates(SlotPhilox(k0, k1, cu.gi, (uint32_t)s_first), g.S, pv);
   const double* hyp_c = a.hyp2 + (int64_t)c * HS;
   for (int64_t it = 0; it < n_sweeps; ++it) {
@@ -1742,9 +1871,7 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
       if (s_abort) return;
     }
     CLV_P_STAMP(a.stamps, wgi, 1, stp);
-    double acc[NS];
-#pragma unroll
-    for (int j = 0; j < NS; ++j) acc[j] = 0.0;
+    StatGen<D, K> st{};
     CustOut<D> out{};
     if (cu.active) {
       cust_coeffs<D, K, false>(cu, Hs, exp_tab);
@@ -1754,10 +1881,19 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
       if (pre) mh_run_pre(cu, pv, s00, s11, g.S, exp_tab);
       else mh_run(cu, SlotPhilox(k0, k1, cu.gi, (uint32_t)s), s00, s11, g.S, exp_tab);
       CLV_P_STAMP(a.stamps, wgi, 3, stp);
-      out = cust_finish<D, K, false, NS>(cu, a, s, stored, Hs, k0, k1, nullptr, exp_tab, acc);
+      out = cust_finish<D, K, false>(cu, a, s, stored, Hs, k0, k1, nullptr, exp_tab, st);
     }
     CLV_P_STAMP(a.stamps, wgi, 4, stp);
-    block_reduce<NS>(acc, red, tot);
+#if PERSIST_REDUCE_GEN
+    block_reduce_gen<NS, SWEEP_REDUCE_CHUNK>(st, red, tot);
+#else
+    {
+      double acc[NS];
+#pragma unroll
+      for (int j = 0; j < NS; ++j) acc[j] = st(j);
+      block_reduce<NS>(acc, red, tot);
+    }
+#endif
     if (tid < NS) st_wt(parts + (int64_t)tid * g.blocks_per_rank + b, tot[tid]);
     CLV_P_STAMP(a.stamps, wgi, 5, stp);
     CLV_P_STAMP(a.stamps, wgi, 8, stp);
@@ -1929,8 +2065,13 @@ hipError_t launch_sweep(const SweepArgs& a, bool replay, hipStream_t st, hipEven
   // (no extra marker packets in the stream, unlike hipEventRecord around the launch).
 #define CLV_CASE(DD, KK, RR)                                                                      \
   if (a.g.D == DD && a.g.K == KK && replay == RR) {                                               \
-    if (e0) hipExtLaunchKernelGGL((sweep_kernel<DD, KK, RR>), grid, block, 0, st, e0, e1, 0, a); \
-    else hipLaunchKernelGGL((sweep_kernel<DD, KK, RR>), grid, block, 0, st, a);                   \
+    if (SweepOcc<DD, KK>::value >= 4) {                                                           \
+      if (e0) hipExtLaunchKernelGGL((sweep_kernel_occ4<DD, KK, RR>), grid, block, 0, st, e0, e1, 0, a); \
+      else hipLaunchKernelGGL((sweep_kernel_occ4<DD, KK, RR>), grid, block, 0, st, a);            \
+    } else {                                                                                      \
+      if (e0) hipExtLaunchKernelGGL((sweep_kernel<DD, KK, RR>), grid, block, 0, st, e0, e1, 0, a); \
+      else hipLaunchKernelGGL((sweep_kernel<DD, KK, RR>), grid, block, 0, st, a);                 \
+    }                                                                                             \
     return hipGetLastError();                                                                     \
   }
   CLV_FOR_K(CLV_CASE, 2, false)

@@ -35,12 +35,23 @@ def _ref_run(p, sweeps, kw):
 
 @pytest.mark.parametrize("D,covs,n,world,sink", [(2, ["first_sales_scaled"], 23570, 2, "summary"),
                                                  (3, ["gender_F", "age_scaled"], 23570, 3, "full"),
-                                                 (2, [], 2357, 2, "full")])
+                                                 (2, [], 2357, 2, "full"),
+                                                 # c4's instance (bivariate K=5, persist_kernel<2,5,true>)
+                                                 # and c5's (trivariate K=9): synthetic covariates
+                                                 (2, ["c1", "c2", "c3", "c4"], 40000, 2, "summary"),
+                                                 (3, [f"c{k}" for k in range(1, 9)], 20000, 2, "summary")])
 def test_p2p_persistent_bitwise_equals_unsharded(D, covs, n, world, sink):
+    """K = 5 / 9 at world 2 on one card: the driver's 8-GPU c4 layout (125k customers per rank)
+    would need 8 x 490 workgroups resident on ONE GPU at once, so the instance is checked here at
+    the largest size whose two grids fit one card together."""
     import torch
     from mcmc_clv_model_amd import distributed as Dm
+    from mcmc_clv_model_amd.data import synthetic_cbs
     from mcmc_clv_model_amd.sampler import HipSampler, build_problem, make_prior
-    df = cdnow("full", n) if n > 2357 else cdnow("abe", n)
+    if covs and covs[0] == "c1":
+        df = synthetic_cbs(n, len(covs) + 1, D, seed=n)
+    else:
+        df = cdnow("full", n) if n > 2357 else cdnow("abe", n)
     p = build_problem(df, covs, D)
     kw = dict(mcmc=9, burnin=4, thin=2, chains=2, seed=4242, draw_sink=sink)
     chunks = (1, 5, 7)

@@ -324,17 +324,22 @@ def test_sharded_path_bitwise_equals_unsharded(L, D, covs, n):
             sh.close()
 
 
-def test_full_size_c5_eight_shards_bitwise(L):
-    """Maximum size: the whole 10M-customer trivariate K=9 problem on one GPU, and
-    the same problem as the driver's 8-GPU layout — 8 shards of 1.25M customers through the
-    sharded C path on one card — agree bit for bit after 3 sweeps (state, summary sums, level-2
-    draws, log-likelihood): size-independent parity at the full c5 size (64-bit indexing, 39,063
-    blocks, 512-unit exchange)."""
+@pytest.mark.parametrize("cfg", ["c4", "c5"])
+def test_full_size_eight_shards_bitwise(L, cfg):
+    """Maximum sizes: c5 — the whole 10M-customer trivariate K=9 problem — and c4 —
+    1M bivariate customers, K=5 — on one GPU, and the same problem as the driver's 8-GPU layout
+    (8 shards of 1.25M / 125k customers through the sharded C path on one card) agree bit for bit
+    after 3 sweeps (state, summary sums, level-2 draws, log-likelihood): size-independent parity
+    at the full sizes (64-bit indexing, 39,063 / 3,907 blocks, 512-unit exchange); plus the
+    posterior moments' sanity (finite, P(alive) in [0, 1])."""
     import torch
     from mcmc_clv_model_amd import distributed as Dm
     from mcmc_clv_model_amd.data import synthetic_cbs
     from mcmc_clv_model_amd.sampler import HipSampler, build_problem, make_prior
-    p = build_problem(synthetic_cbs(10_000_000, 9, 3, seed=20250719), [f"c{k}" for k in range(1, 9)], 3)
+    if cfg == "c5":
+        p = build_problem(synthetic_cbs(10_000_000, 9, 3, seed=20250719), [f"c{k}" for k in range(1, 9)], 3)
+    else:
+        p = build_problem(synthetic_cbs(1_000_000, 5, 2, seed=20250718), [f"c{k}" for k in range(1, 5)], 2)
     kw = dict(mcmc=2, burnin=1, thin=1, chains=1, seed=20250719, draw_sink="summary")
     sweeps = 3
     with HipSampler(p, **kw) as s:
@@ -343,6 +348,7 @@ def test_full_size_c5_eight_shards_bitwise(L):
         ref_sums, k_ref = s.read_summary()
         _, ref_l2, ref_ll = s.read_draws(level1=False)
     assert k_ref == 2 and np.isfinite(ref_l2).all() and np.isfinite(ref_ll).all()
+    assert np.isfinite(ref_sums).all() and (ref_sums[:, 2] >= 0).all() and (ref_sums[:, 2] <= k_ref).all()
     world = 8
     plan = Dm.plan(p.N, world)
     prior = make_prior(p, p.N)
@@ -354,15 +360,21 @@ def test_full_size_c5_eight_shards_bitwise(L):
                                  blocks_per_unit=plan.blocks_per_unit, prior=prior, **kw))
     nd = shards[0].partials()[1]
     gathered = torch.zeros(nd * world, dtype=torch.float64, device="cuda")
+
+    def exchange_and_hyper():
+        for r, sh in enumerate(shards):
+            sh.copy_partials(gathered.data_ptr() + r * nd * 8)
+            sh.synchronize()
+        for sh in shards:
+            sh.hyper(gathered.data_ptr())
+
     try:
-        for _ in range(sweeps):  # trivariate: the level-2 draw closes each sweep
+        if p.D == 2:  # bivariate: the initial draw from the initial state (bi:393 at step 1)
+            exchange_and_hyper()
+        for _ in range(sweeps):  # the level-2 draw closes each sweep
             for sh in shards:
                 sh.sweep()
-            for r, sh in enumerate(shards):
-                sh.copy_partials(gathered.data_ptr() + r * nd * 8)
-                sh.synchronize()
-            for sh in shards:
-                sh.hyper(gathered.data_ptr())
+            exchange_and_hyper()
         for r, sh in enumerate(shards):
             sh.synchronize()
             b, e = plan.shard(r)

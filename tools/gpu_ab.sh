@@ -11,7 +11,7 @@ if [ "${TESTS:-0}" = "1" ]; then
 fi
 for W in "$@"; do
   for V in $VALS; do
-    env $VAR=$V timeout -k 10 300 python bench.py --workload $W --no-cpu-baseline --steps ${STEPS:-5000} --warmup 300 \
+    env $VAR=$V timeout -k 10 300 python bench.py --workload $W --no-cpu-baseline --scaling-configs "" --steps ${STEPS:-5000} --warmup 300 \
       --timing-steps 1000 > gpurun_out/ab_${W}_${V}.log 2>&1; rc=$?
     echo ${W}_${VAR}=${V}_rc=$rc; python - "gpurun_out/ab_${W}_${V}.log" <<'PY'
 import json,sys
