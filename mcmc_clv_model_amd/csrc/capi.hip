@@ -75,10 +75,7 @@ SweepArgs sweep_args(clv_sampler* s, int init, int fuse = 0) {
   a.hyper_out = s->d_hyper_alt ? s->d_hyper_alt : s->d_hyper;
   a.wait_ticks = s->wait_ticks;
   a.abort_host = s->d_h_abort;
-  {  // CLV_PRE_VARIATES=0: draw the MH variates inside the MH phase (A/B measurements)
-    const char* env = std::getenv("CLV_PRE_VARIATES");
-    a.pre_variates = (env && std::string(env) == "0") ? 0 : 1;
-  }
+  a.pre_variates = s->pre_variates;
   a.h = hyper_args(s, nullptr, 0);
   if (fuse) a.h.hvar = s->replay ? nullptr : s->d_hvar;
   return a;
@@ -443,6 +440,12 @@ int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* pri
     const double ms = env ? std::atof(env) : (cfg->world_size > 1 ? 10000.0 : 2000.0);
     s->wait_ticks = (uint64_t)(std::max(1.0, ms) * 1e5);  // s_memrealtime: 100 MHz
   }
+  {
+    const char* env = std::getenv("CLV_SYNC");
+    if (env) s->sync_mode = std::max(0, std::min(2, std::atoi(env)));
+    env = std::getenv("CLV_PRE_VARIATES");  // 0: MH variates drawn inside the MH phase (A/B)
+    s->pre_variates = (env && std::string(env) == "0") ? 0 : 1;
+  }
   if ((s->persistent || s->p2p_capable) && s->n_cu > 0) {
     // default on for the bivariate model only: measured c2 13.44 -> 12.94 us per sweep, but c3
     // (trivariate: longer level-2 draw, so both waves of a same-chain pair idle in the hand-off
@@ -542,6 +545,7 @@ void clv_destroy(clv_sampler* s) {
   if (s->stream) (void)hipStreamSynchronize(s->stream);
   if (s->graph_exec) (void)hipGraphExecDestroy(s->graph_exec);
   for (auto e : s->ev) (void)hipEventDestroy(e);
+  if (s->done_ev) (void)hipEventDestroy(s->done_ev);
   void* ptrs[] = {s->d_x, s->d_tx, s->d_T, s->d_cov, s->d_logs, s->d_lam, s->d_mu, s->d_hyper,
                   s->d_block, s->d_prior, s->d_ctrl, s->d_level1, s->d_level2, s->d_loglik,
                   s->d_sums, s->d_tape, s->d_bs, s->d_arrive, s->d_hvar, s->d_stamps};
@@ -752,12 +756,29 @@ int run_persistent(clv_sampler* s, int64_t n_sweeps) {
     s->ev_sweeps[s->ev_used] = n_sweeps;
   }
   CLV_HIP(launch_persist(a, s->sweeps_done + 1, n_sweeps, s->stream, e0, e1));
+  // wait for the launch: its end event (timing: the dispatch's own end timestamp; else one
+  // recorded behind it).  Timed launches are harvested later (clv_kernel_time or a full slot set).
+  hipEvent_t done = e1;
   if (s->timing) {
-    s->ev_used++;
-    int rc = harvest_timing(s);
-    if (rc) return rc;
+    if (++s->ev_used == TIMING_EVENTS) {
+      int rc = harvest_timing(s);
+      if (rc) return rc;
+    }
+  } else if (s->sync_mode != 0) {
+    if (!s->done_ev) CLV_HIP(hipEventCreateWithFlags(&s->done_ev, hipEventDisableTiming));
+    CLV_HIP(hipEventRecord(s->done_ev, s->stream));
+    done = s->done_ev;
   }
-  CLV_HIP(hipStreamSynchronize(s->stream));
+  if (s->sync_mode == 0 || !done) {
+    CLV_HIP(hipStreamSynchronize(s->stream));
+  } else if (s->sync_mode == 1) {
+    hipError_t q;
+    while ((q = hipEventQuery(done)) == hipErrorNotReady) {
+    }
+    CLV_HIP(q);
+  } else {
+    CLV_HIP(hipEventSynchronize(done));
+  }
   if (__atomic_load_n(s->h_abort, __ATOMIC_ACQUIRE)) {
     // the carried state was written to the *_alt buffers only: lam / mu / hyper still hold the
     // state this launch started from; restore the counters, flags and running sums

@@ -107,6 +107,12 @@ struct clv_sampler {
   hipGraphExec_t graph_exec = nullptr;
   int graph_sweeps = 0;
 
+  // how clv_run waits for a persistent launch (CLV_SYNC, read at create): 0 hipStreamSynchronize,
+  // 1 poll hipEventQuery on the launch's end event, 2 hipEventSynchronize on it
+  int sync_mode = 1;
+  hipEvent_t done_ev = nullptr;     // recorded after each untimed persistent launch (timing: e1)
+  int pre_variates = 1;             // CLV_PRE_VARIATES (read at create)
+
   bool timing = false;
   std::vector<hipEvent_t> ev;  // 4 per slot: sweep start/end, hyper start/end
   std::vector<int64_t> ev_sweeps;  // sweeps per timed launch (persistent launches time many)

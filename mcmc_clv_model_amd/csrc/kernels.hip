@@ -2055,8 +2055,12 @@ __global__ void debug_mh_kernel(const int32_t* x, const uint8_t* z, const double
 // ---------------------------------------------------------------------------------------------
 // Dispatch
 // ---------------------------------------------------------------------------------------------
+#ifdef CLV_ONLY_K  // analysis builds only (tools/asm_*.py): one covariate count, a fraction of the compile time
+#define CLV_FOR_K(M, D, R) M(D, CLV_ONLY_K, R)
+#else
 #define CLV_FOR_K(M, D, R) \
   M(D, 1, R) M(D, 2, R) M(D, 3, R) M(D, 4, R) M(D, 5, R) M(D, 6, R) M(D, 7, R) M(D, 8, R) M(D, 9, R)
+#endif
 
 hipError_t launch_sweep(const SweepArgs& a, bool replay, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
   const dim3 grid(a.g.nb_local, a.g.n_chains);
