@@ -52,6 +52,7 @@ SweepArgs sweep_args(clv_sampler* s, int init, int fuse = 0) {
   a.mu = s->d_mu;
   a.hyper = s->d_hyper;
   a.blockpart = s->d_block;
+  a.pblock = s->d_pblock;
   a.ctrl = s->d_ctrl;
   a.level1 = s->d_level1;
   a.sums = s->d_sums;
@@ -108,7 +109,6 @@ HyperArgs hyper_args(clv_sampler* s, const double* units, int mode) {
 }
 
 int enqueue_sweep(clv_sampler* s, hipEvent_t e0, hipEvent_t e1) {
-  s->slots_dirty = true;  // block partials written (the persistent hand-off needs its sentinel fill)
   s->last_persist_n = 0;
   CLV_HIP(launch_sweep(sweep_args(s, 0), s->replay, s->stream, e0, e1));
   if (s->g.blocks_per_unit > 1) {
@@ -123,7 +123,6 @@ int enqueue_sweep(clv_sampler* s, hipEvent_t e0, hipEvent_t e1) {
 
 // world_size == 1: one launch per sweep (the level-2 draw runs in the sweep kernel's tail)
 int enqueue_fused(clv_sampler* s, hipEvent_t e0, hipEvent_t e1) {
-  s->slots_dirty = true;
   s->last_persist_n = 0;
   CLV_HIP(launch_sweep(sweep_args(s, 0, 1), s->replay, s->stream, e0, e1));
   return CLV_OK;
@@ -426,6 +425,7 @@ int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* pri
     }
   }
   if (s->persistent || s->p2p_capable) {
+    CLV_HIPC(dalloc(&s->d_pblock, (size_t)C * nb_local * g.stride));
     CLV_HIPC(dalloc(&s->d_lam_alt, C * std::max<int64_t>(n, 1)));
     CLV_HIPC(dalloc(&s->d_mu_alt, C * std::max<int64_t>(n, 1)));
     CLV_HIPC(dalloc(&s->d_hyper_alt, C * HS));
@@ -553,7 +553,8 @@ void clv_destroy(clv_sampler* s) {
     if (p) (void)hipFree(p);
   if (s->d_unit && s->d_unit != s->d_block) (void)hipFree(s->d_unit);
   if (s->d_hyp2) (void)hipFree(s->d_hyp2);
-  for (void* p : {(void*)s->d_lam_alt, (void*)s->d_mu_alt, (void*)s->d_hyper_alt, (void*)s->d_sums_prev})
+  for (void* p : {(void*)s->d_lam_alt, (void*)s->d_mu_alt, (void*)s->d_hyper_alt, (void*)s->d_sums_prev,
+                  (void*)s->d_pblock})
     if (p) (void)hipFree(p);
   if (s->h_abort) (void)hipHostFree(s->h_abort);
   for (void* p : s->ipc_opened) (void)hipIpcCloseMemHandle(p);
@@ -736,10 +737,7 @@ int run_persistent(clv_sampler* s, int64_t n_sweeps) {
   if (s->slots_dirty) {  // a completed launch leaves every hand-off slot empty; else fill them
     // every hand-off slot empty (all-ones bytes: the sentinel NaN)
     CLV_HIP(hipMemsetAsync(s->d_hyp2, 0xFF, sizeof(double) * 2 * g.n_chains * HS, s->stream));
-    // (only the nb_local live columns of each [chain][stat] row: padding blocks stay 0.0 for the
-    // group kernel of the sharded path)
-    CLV_HIP(hipMemset2DAsync(s->d_block, sizeof(double) * g.blocks_per_rank, 0xFF, sizeof(double) * g.nb_local,
-                             (size_t)g.n_chains * g.stride, s->stream));
+    CLV_HIP(hipMemsetAsync(s->d_pblock, 0xFF, sizeof(double) * g.n_chains * g.nb_local * g.stride, s->stream));
     s->slots_dirty = false;
   }
   const size_t sums_bytes = sizeof(double) * (size_t)g.n_chains * CLV_N_SUM_STATS * g.n;

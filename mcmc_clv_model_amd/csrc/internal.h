@@ -74,6 +74,7 @@ struct clv_sampler {
   clv::Ctrl* d_ctrl = nullptr;
   uint32_t* d_arrive = nullptr;     // fused-tail arrival counters: [chain], then [chain][units_per_rank]
   double* d_hyp2 = nullptr;         // persistent kernel: [2][chain][HS] hand-off slots
+  double* d_pblock = nullptr;       // persistent kernel: [chain][nb_local][stride] block-partial slots
   // persistent kernel: the launch writes its carried state into the *_alt buffers; clv_run swaps
   // them in only when no wave aborted (an aborted launch leaves the state untouched), and
   // clv_rollback swaps them back (a sharded step that failed on another rank)
@@ -82,15 +83,15 @@ struct clv_sampler {
   uint32_t* h_abort = nullptr;      // host-mapped copy of ctrl->abort (the kernel stores it on a timeout)
   uint32_t* d_h_abort = nullptr;    // its device address
   uint64_t wait_ticks = 0;          // bound on every persistent-kernel wait (s_memrealtime ticks)
-  bool slots_dirty = true;          // hand-off slots need the sentinel fill (a completed persistent
-                                    // launch leaves them empty; sweep kernels write block partials)
+  bool slots_dirty = true;          // persistent hand-off slots need the sentinel fill (a completed
+                                    // launch leaves them empty; only an aborted one does not)
   int64_t last_persist_n = 0;       // sweeps of the last persistent launch (rollback), 0 = none
   bool persistent = false;          // clv_run uses persist_kernel (all workgroups resident)
   int persist_bpc = 0, n_cu = 0;    // persist_kernel occupancy (workgroups per CU), CUs
   // world size > 1: persistent kernel with the peer (xGMI) exchange
   bool p2p_capable = false;         // the grid fits at once and the unit partials fit UMAIL
   bool p2p_ready = false;           // clv_p2p_connect done: clv_run runs persist_kernel
-  double* d_mail = nullptr;         // [2][world][chain][stride][units_per_rank]
+  double* d_mail = nullptr;         // [2][world][chain][units_per_rank][stride]
   double** d_peers = nullptr;       // [world] mail pointers (peers' opened IPC mappings, own d_mail)
   int32_t* d_wgmap = nullptr;       // persistent grid: linear workgroup -> (chain << 16 | block)
   std::vector<void*> ipc_opened;    // hipIpcOpenMemHandle mappings to close

@@ -87,6 +87,7 @@ struct SweepArgs {
   double* mu;
   const double* hyper;       // [chain][HS]
   double* blockpart;         // [chain][stride][blocks_per_rank]
+  double* pblock;            // persistent kernel: [chain][nb_local][stride] hand-off slots
   const Ctrl* ctrl;
   Ctrl* ctrl_rw;             // persistent kernel: writes cur and abort
   double* hyp2;              // persistent kernel: [2][chain][HS] (beta, Sigma) hand-off slots by sweep parity
@@ -102,7 +103,7 @@ struct SweepArgs {
   double* hvar_out;          // [chain][HV]: the chain's last workgroup precomputes the next level-2
                              // draw's Philox variates at its start (off the critical path), or null
   // persistent kernel at world size > 1 (peer exchange over xGMI): unit partials of sweep s go
-  // straight into every rank's mail buffer, [2 (sweep parity)][world][chain][stride][units_per_rank]
+  // straight into every rank's mail buffer, [2 (sweep parity)][world][chain][units_per_rank][stride]
   double* mail;              // this rank's mail buffer (device memory, polled by its level-2 workgroups)
   double* const* peers;      // [world] device pointers to every rank's mail buffer (peers[rank] = mail)
   int rank;

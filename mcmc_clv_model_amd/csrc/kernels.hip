@@ -20,6 +20,13 @@
 #ifndef SWEEP_MH_PIPELINE
 #define SWEEP_MH_PIPELINE 1  // 1: next MH chunk's variates drawn during the current chunk's steps
 #endif
+// register-pressure knobs of the persistent kernel (A/B builds override them):
+#ifndef CLV_OPAQUE_GI
+#define CLV_OPAQUE_GI(D) ((D) == 3)   // customer Philox products recomputed per sweep (not hoisted)
+#endif
+#ifndef CLV_L2_OPAQUE
+#define CLV_L2_OPAQUE(P) (P)          // level-2 lane bookkeeping recomputed per sweep (not hoisted)
+#endif
 #ifndef PERSIST_REDUCE_GEN
 #define PERSIST_REDUCE_GEN 1  // persistent kernel: statistics formed chunk-wise in the reduction
 #endif
@@ -620,7 +627,7 @@ __device__ __forceinline__ void iw_core_fast(const double (&Sn)[D][D], const dou
 // element-parallel phases of level2_draw_exact around the fast core.  `Ai`: the Bartlett inverse
 // if already formed (LDS), else null.  Every path (fused, sharded, persistent) calls this same
 // function in Philox mode, so they stay bitwise identical.
-template <int D, int K>
+template <int D, int K, int LANE0_MAX = 12>
 __device__ void level2_draw_fast(const double* tot, const double* iwn, const double* chi2, const double* noise,
                                  const double* Ai_pre, L2Scratch* sc) {
   constexpr int NXY = K * D;
@@ -630,7 +637,7 @@ __device__ void level2_draw_fast(const double* tot, const double* iwn, const dou
   const double* cholV = sc->prior + 81;
   const double* A0B0 = sc->prior + 162;
   const double* S0B = sc->prior + 189;
-  if constexpr (NXY <= 12) {
+  if constexpr (NXY <= LANE0_MAX) {  // (both forms form the same sums in the same order)
     if (t == 0) {
       double Ai[D * D];
       if (Ai_pre) {
@@ -664,6 +671,7 @@ __device__ void level2_draw_fast(const double* tot, const double* iwn, const dou
         }
       double Sig[D][D], M[D][D];
       iw_core_fast<D>(Sn, Ai, Sig, M);
+      asm volatile("" ::: "memory");  // chol(V) and the noise are read here, not hoisted above (registers)
 #pragma unroll
       for (int q = 0; q < NXY; ++q) {  // beta = B_hat + kron(chol Sigma, chol V) z, row-major ravel (Q1)
         const int p = q / K, bq = q % K;
@@ -745,12 +753,12 @@ __device__ void level2_draw_fast(const double* tot, const double* iwn, const dou
 
 // Level-2 draw: replay mode follows the reference's operation order (level2_draw_exact, bitwise
 // trajectories); Philox mode takes the latency-optimised form.
-template <int D, int K>
+template <int D, int K, int LANE0_MAX = 12>
 __device__ __forceinline__ void level2_draw(const double* tot, const double* iwn, const double* chi2,
                                             const double* noise, bool noise_is_w, L2Scratch* sc,
                                             const double* Ai_pre = nullptr) {
   if (noise_is_w) level2_draw_exact<D, K>(tot, iwn, chi2, noise, true, sc);
-  else level2_draw_fast<D, K>(tot, iwn, chi2, noise, Ai_pre, sc);
+  else level2_draw_fast<D, K, LANE0_MAX>(tot, iwn, chi2, noise, Ai_pre, sc);
 }
 
 // Philox-mode hyper variates (fp64).
@@ -1548,12 +1556,12 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
   __shared__ L2Scratch l2;
   __shared__ double* s_peers[P2P ? MAX_WORLD : 1];  // every rank's mail (loaded once)
   const Geometry& g = a.g;
-  const int tid = threadIdx.x;
+  const int tid0 = threadIdx.x;
   (void)wgi;
-  double* parts = a.blockpart + (int64_t)c * g.stride * g.blocks_per_rank;  // [stat][block]
-  if (tid == 0) s_abort = 0;
+  double* parts0 = a.pblock + (int64_t)c * g.nb_local * NS;  // [block][stat]
+  if (tid0 == 0) s_abort = 0;
   if constexpr (P2P) {
-    if (tid < g.world_size) s_peers[tid] = a.peers[tid];
+    if (tid0 < g.world_size) s_peers[tid0] = a.peers[tid0];
   }
   __syncthreads();
   // ================= the chain's level-2 workgroup =================
@@ -1562,6 +1570,14 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
   __builtin_amdgcn_s_setprio(3);
   stage_prior(a.h.V, &l2);
   for (int64_t it = 0; it < n_sweeps; ++it) {
+    // the lane's addresses and unit bookkeeping are recomputed every sweep from an opaque copy of
+    // the lane index (a few integer ops), not kept live across the loop: registers for the phases
+    int tid = tid0;
+    double* parts = parts0;
+    if constexpr (CLV_L2_OPAQUE(P2P)) {
+      asm volatile("" : "+v"(tid));
+      asm volatile("" : "+s"(parts));
+    }
     const int64_t s = s_first + it;
     const bool stp = tid == 0 && it == it_stamp;
     (void)stp;
@@ -1574,20 +1590,31 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
     __syncthreads();
     if (tid == 0) bartlett_inverse<D>(var_iw, var_chi, l2.Ai);  // read back by this lane only
     CLV_P_STAMP(a.stamps, wgi, 1, stp);
-    // 2. wait for every block partial of sweep s (lane tid: blocks tid, tid + NT, ...; nb <= 2 NT)
+    // 2. wait for every block partial of sweep s (lane tid: blocks tid, tid + NT; nb <= 2 NT).
+    //    The persistent kernel's partials are [block][stat]: one base address per block and the
+    //    statistics at immediate offsets (no per-statistic 64-bit addresses held across the poll).
     double v0[NS], v1[NS];
     const int b0 = tid, b1 = tid + NT;
+    const bool hb0 = b0 < g.nb_local, hb1 = b1 < g.nb_local;
+    double* pb0 = parts + (int64_t)b0 * NS;
+    double* pb1 = parts + (int64_t)b1 * NS;
+    // polled unconditionally (no branch per load): lanes without a block / unit read block 0 /
+    // their own first mail slot and discard it
+    const double* qb0 = hb0 ? pb0 : parts;
+    const double* qb1 = hb1 ? pb1 : parts;
     // P2P: the global units this lane sums (u0, u1: as hyper_body, n_units_global <= 2 NT) and
-    // where they come from — another rank's (the mail) or this rank's own (LDS, formed below)
+    // where they come from — another rank's (the mail, [unit][stat]) or this rank's own (LDS, below)
     const int64_t per_rank = (int64_t)g.n_chains * NS * g.units_per_rank;  // mail doubles per rank and parity
     const double* mb = a.mail + (int64_t)(s & 1) * g.world_size * per_rank + (int64_t)c * NS * g.units_per_rank;
     const int64_t u0 = tid, u1 = tid + NT;
     const int r0 = (int)(u0 / g.units_per_rank), r1 = (int)(u1 / g.units_per_rank);
     const int l0 = (int)(u0 % g.units_per_rank), l1 = (int)(u1 % g.units_per_rank);
-    const double* p0 = mb + r0 * per_rank + l0;
-    const double* p1 = mb + r1 * per_rank + l1;
+    const double* p0 = mb + r0 * per_rank + (int64_t)l0 * NS;
+    const double* p1 = mb + r1 * per_rank + (int64_t)l1 * NS;
     const bool h0 = u0 < g.n_units_global, h1 = u1 < g.n_units_global;
     const bool m0 = P2P && h0 && r0 != a.rank, m1 = P2P && h1 && r1 != a.rank;
+    const double* q0 = m0 ? p0 : mb;
+    const double* q1 = m1 ? p1 : mb;
     double w0[NS], w1[NS];
     bool mdone = !(m0 || m1);  // this lane's mail slots all full (or none to read)
     {  // each wavefront polls on its own (no barrier per poll); a lane stops once its slots are full.
@@ -1600,11 +1627,11 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
           bool ok = true;
 #pragma unroll
           for (int j = 0; j < NS; ++j) {
-            v0[j] = b0 < g.nb_local ? ld_wt(parts + (int64_t)j * g.blocks_per_rank + b0) : 0.0;
-            v1[j] = b1 < g.nb_local ? ld_wt(parts + (int64_t)j * g.blocks_per_rank + b1) : 0.0;
+            v0[j] = ld_wt(qb0 + j);
+            v1[j] = ld_wt(qb1 + j);
           }
 #pragma unroll
-          for (int j = 0; j < NS; ++j) ok = ok && slot_full(v0[j]) && slot_full(v1[j]);
+          for (int j = 0; j < NS; ++j) ok = ok & (!hb0 | slot_full(v0[j])) & (!hb1 | slot_full(v1[j]));
           done = ok;
         }
         if constexpr (P2P) {
@@ -1612,11 +1639,11 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
             bool ok = true;
 #pragma unroll
             for (int j = 0; j < NS; ++j) {
-              w0[j] = m0 ? ld_sys(p0 + (int64_t)j * g.units_per_rank) : 0.0;
-              w1[j] = m1 ? ld_sys(p1 + (int64_t)j * g.units_per_rank) : 0.0;
+              w0[j] = ld_sys(q0 + j);
+              w1[j] = ld_sys(q1 + j);
             }
 #pragma unroll
-            for (int j = 0; j < NS; ++j) ok = ok && slot_full(w0[j]) && slot_full(w1[j]);
+            for (int j = 0; j < NS; ++j) ok = ok & (!m0 | slot_full(w0[j])) & (!m1 | slot_full(w1[j]));
             mdone = ok;
           }
         }
@@ -1630,6 +1657,11 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
     }
     __syncthreads();
     if (s_abort) return;
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {  // padding blocks contribute 0.0 (group_kernel's zero padding)
+      v0[j] = hb0 ? v0[j] : 0.0;
+      v1[j] = hb1 ? v1[j] : 0.0;
+    }
     CLV_P_STAMP(a.stamps, wgi, 2, stp);
     // 3. the fused path's fixed-order sum (hyper_body: lane u sums units u, u + NT, ... in order)
     double acc[NS];
@@ -1637,57 +1669,50 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
 #pragma unroll
       for (int j = 0; j < NS; ++j) {
         acc[j] = 0.0;
-        if (b0 < g.nb_local) acc[j] += v0[j];
-        if (b1 < g.nb_local) acc[j] += v1[j];
+        if (hb0) acc[j] += v0[j];
+        if (hb1) acc[j] += v1[j];
       }
     } else {
-      double* umail = pool;  // [UMAIL]: this rank's unit partials [stat][local unit] (the pool the
+      double* umail = pool;  // [UMAIL]: this rank's unit partials [local unit][stat] (the pool the
                              // customer workgroups use for their drawn-ahead MH variates)
       // 3a. this rank's unit partials: blocks_per_unit consecutive blocks summed in group_kernel's
       //     order (a unit's blocks sit in consecutive lanes of one wavefront: bpu | 64); with one
       //     block per unit the unit partial IS the block partial (the sharded path has no group
-      //     kernel then)
+      //     kernel then).  One half (blocks tid / tid + NT) at a time: fewer live registers.
       const int bpu = g.blocks_per_unit;
       const int ul = (g.nb_local + bpu - 1) / bpu;
       const int lane = tid & 63;
-      double t0[NS], t1[NS];
-      if (bpu == 1) {
 #pragma unroll
-        for (int j = 0; j < NS; ++j) {
-          t0[j] = v0[j];
-          t1[j] = v1[j];
-        }
-      } else {
+      for (int half = 0; half < 2; ++half) {
+        const double* v = half ? v1 : v0;
+        const int ub = (tid + half * NT) / bpu;  // this lane's local unit (if it leads one)
+        double t[NS];
+        if (bpu == 1) {
 #pragma unroll
-        for (int j = 0; j < NS; ++j) {
-          t0[j] = 0.0 + v0[j];
-          t1[j] = 0.0 + v1[j];
-        }
-        for (int k = 1; k < bpu; ++k) {  // all statistics' shuffles of one k in flight together
+          for (int j = 0; j < NS; ++j) t[j] = v[j];
+        } else {
 #pragma unroll
-          for (int j = 0; j < NS; ++j) {
-            t0[j] += __shfl(v0[j], lane + k, 64);  // blocks >= nb_local contribute 0.0, as
-            t1[j] += __shfl(v1[j], lane + k, 64);  // group_kernel's zero-initialised padding does
-          }
-        }
-      }
-      if (tid % bpu == 0) {
+          for (int j = 0; j < NS; ++j) t[j] = 0.0 + v[j];
+          for (int k = 1; k < bpu; ++k) {  // all statistics' shuffles of one k in flight together
 #pragma unroll
-        for (int j = 0; j < NS; ++j) {
-          if (tid / bpu < ul) umail[j * ul + tid / bpu] = t0[j];
-          if ((tid + NT) / bpu < ul) umail[j * ul + (tid + NT) / bpu] = t1[j];
+            for (int j = 0; j < NS; ++j) t[j] += __shfl(v[j], lane + k, 64);  // blocks >= nb_local
+          }                                                                  // add 0.0, as
+        }                                                                    // group_kernel's padding
+        if (tid % bpu == 0 && ub < ul) {
+#pragma unroll
+          for (int j = 0; j < NS; ++j) umail[ub * NS + j] = t[j];
         }
       }
       lds_barrier();
       CLV_P_STAMP(a.stamps, wgi, 10, stp);
       // 3b. to every OTHER rank's mail slot of sweep s (write-through stores over xGMI; the value
-      //     is its own arrival flag — the sentinel never occurs in a partial); own units stay in LDS
+      //     is its own arrival flag — the sentinel never occurs in a partial); own units stay in
+      //     LDS.  [unit][stat] on both sides: consecutive lanes store consecutive doubles.
       const int64_t dst = ((int64_t)(s & 1) * g.world_size + a.rank) * per_rank + (int64_t)c * NS * g.units_per_rank;
       for (int e = tid; e < NS * ul; e += NT) {
-        const int j = e / ul, lu = e - j * ul;
         const double v = umail[e];
         for (int q = 0; q < g.world_size; ++q)
-          if (q != a.rank) st_sys(s_peers[q] + dst + (int64_t)j * g.units_per_rank + lu, v);
+          if (q != a.rank) st_sys(s_peers[q] + dst + e, v);
       }
       // 3c. the other ranks' units not seen yet
       const uint64_t tw = __builtin_amdgcn_s_memrealtime();
@@ -1696,11 +1721,11 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
           bool ok = true;
 #pragma unroll
           for (int j = 0; j < NS; ++j) {
-            w0[j] = m0 ? ld_sys(p0 + (int64_t)j * g.units_per_rank) : 0.0;
-            w1[j] = m1 ? ld_sys(p1 + (int64_t)j * g.units_per_rank) : 0.0;
+            w0[j] = ld_sys(q0 + j);
+            w1[j] = ld_sys(q1 + j);
           }
 #pragma unroll
-          for (int j = 0; j < NS; ++j) ok = ok && slot_full(w0[j]) && slot_full(w1[j]);
+          for (int j = 0; j < NS; ++j) ok = ok & (!m0 | slot_full(w0[j])) & (!m1 | slot_full(w1[j]));
           mdone = ok;
         }
         if (__all(mdone)) break;
@@ -1715,8 +1740,8 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
       if (s_abort) return;
 #pragma unroll
       for (int j = 0; j < NS; ++j) {
-        const double x0 = m0 ? w0[j] : (h0 ? umail[j * ul + l0] : 0.0);
-        const double x1 = m1 ? w1[j] : (h1 ? umail[j * ul + l1] : 0.0);
+        const double x0 = m0 ? w0[j] : (h0 ? umail[l0 * NS + j] : 0.0);
+        const double x1 = m1 ? w1[j] : (h1 ? umail[l1 * NS + j] : 0.0);
         acc[j] = 0.0;
         if (h0) acc[j] += x0;
         if (h1) acc[j] += x1;
@@ -1728,8 +1753,8 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
     //    (beta, Sigma) set every reader of s has read (its next write is for s+2)
 #pragma unroll
     for (int j = 0; j < NS; ++j) {
-      if (b0 < g.nb_local) st_wt(parts + (int64_t)j * g.blocks_per_rank + b0, slot_empty());
-      if (b1 < g.nb_local) st_wt(parts + (int64_t)j * g.blocks_per_rank + b1, slot_empty());
+      if (hb0) st_wt(pb0 + j, slot_empty());
+      if (hb1) st_wt(pb1 + j, slot_empty());
     }
     if (it > 0 && tid < HS) st_wt(a.hyp2 + ((int64_t)(s & 1) * g.n_chains + c) * HS + tid, slot_empty());
     if constexpr (P2P) {  // this rank's mail slots of sweep s: empty again before any rank can
@@ -1737,13 +1762,15 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
                           // leave after the vmcnt(0) below)
 #pragma unroll
       for (int j = 0; j < NS; ++j) {
-        if (m0) st_sys((double*)p0 + (int64_t)j * g.units_per_rank, slot_empty());
-        if (m1) st_sys((double*)p1 + (int64_t)j * g.units_per_rank, slot_empty());
+        if (m0) st_sys((double*)p0 + j, slot_empty());
+        if (m1) st_sys((double*)p1 + j, slot_empty());
       }
     }
     if (tid < HS) Hs[tid] = 0.0;  // unwritten hyper slots publish as 0 (wavefront 0: ordered before the draw's writes)
     // 5. the draw (wavefront 0) while the resets drain
-    level2_draw<D, K>(tot, var_iw, var_chi, var_noise, false, &l2, l2.Ai);
+    // P2P: the one-lane form only for the smallest K*D (its registers, added to the exchange's,
+    // spilled the peer kernel at K*D = 10); the element-parallel form gives the same bits
+    level2_draw<D, K, P2P ? 6 : 12>(tot, var_iw, var_chi, var_noise, false, &l2, l2.Ai);
     CLV_P_STAMP(a.stamps, wgi, 7, stp);
     if (tid == 0) {
       double Sig[D][D];
@@ -1819,7 +1846,7 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
   (void)it_stamp;
   uint32_t k0, k1;
   chain_key(a.r.seed, (int64_t)a.r.chain_first + c, &k0, &k1);
-  double* parts = a.blockpart + (int64_t)c * g.stride * g.blocks_per_rank;  // [stat][block]
+  double* parts = a.pblock + (int64_t)c * g.nb_local * NS;  // [block][stat]
   if (tid == 0) s_abort = 0;
 
   if (b == g.nb_local) {  // the chain's level-2 workgroup
@@ -1845,6 +1872,9 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
   if (cu.active && pre) mh_pre_variates(SlotPhilox(k0, k1, cu.gi, (uint32_t)s_first), g.S, pv);
   const double* hyp_c = a.hyp2 + (int64_t)c * HS;
   for (int64_t it = 0; it < n_sweeps; ++it) {
+    // Philox products of the customer counter word are the same every sweep; hoisted out of the
+    // loop they were kept live (and spilled, tri K=3) — recomputed per sweep instead (a few VALU)
+    if constexpr (CLV_OPAQUE_GI(D)) asm volatile("" : "+v"(cu.gi));
     const int64_t s = s_first + it;
     const bool stored = is_stored(s, g);
     const bool stp = tid == 0 && it == it_stamp;
@@ -1894,7 +1924,7 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
       block_reduce<NS>(acc, red, tot);
     }
 #endif
-    if (tid < NS) st_wt(parts + (int64_t)tid * g.blocks_per_rank + b, tot[tid]);
+    if (tid < NS) st_wt(parts + (int64_t)b * NS + tid, tot[tid]);  // one contiguous 8*NS-byte record
     CLV_P_STAMP(a.stamps, wgi, 5, stp);
     CLV_P_STAMP(a.stamps, wgi, 8, stp);
     CLV_P_STAMP(a.stamps, wgi, 9, stp);
