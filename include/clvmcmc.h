@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define CLV_ABI_VERSION 1
+#define CLV_ABI_VERSION 2
 
 /* Customers per workgroup == the sufficient-statistic block size. Shards must begin on a
  * multiple of it so block partial sums are identical for every GPU count. */
@@ -39,13 +39,20 @@ extern "C" {
 
 enum { CLV_OK = 0, CLV_EINVAL = -1, CLV_EHIP = -2, CLV_ESTATE = -3, CLV_ENOMEM = -4 };
 enum { CLV_RNG_PHILOX = 0, CLV_RNG_REPLAY = 1 };
-enum { CLV_SINK_FULL = 0, CLV_SINK_SUMMARY = 1, CLV_SINK_NONE = 2 };
+/* CLV_SINK_SUMMARY_PCT: the summary sums plus every stored (lambda, mu) as a float32 pair,
+ * [chain][draw][n] (8 B per customer and stored sweep instead of the full sink's 8 (D+2)), from
+ * which clv_level1_summary_sampler forms the per-customer 2.5 / 97.5 percentiles of Table 4
+ * (analysis_bi_helpers.py:95-96, 116-117): exact order statistics of the float32-rounded draws. */
+enum { CLV_SINK_FULL = 0, CLV_SINK_SUMMARY = 1, CLV_SINK_NONE = 2, CLV_SINK_SUMMARY_PCT = 3 };
 
-/* Per-customer running sums kept on device by CLV_SINK_SUMMARY (and readable in any mode),
- * accumulated over stored draws. Layout of clv_read_summary(): [chain][stat][n]. */
+/* Per-customer running sums kept on device by CLV_SINK_SUMMARY / _PCT, accumulated over stored
+ * draws. Layout of clv_read_summary(): [chain][stat][n].  CLV_SUM_MU_CAPPED sums
+ * min(mu, CLV_SUMMARY_MU_CAP): Table 4's capped posterior mean of mu (analysis_bi_helpers.py:88-93). */
+#define CLV_SUMMARY_MU_CAP 0.05
 enum {
   CLV_SUM_LAMBDA = 0, CLV_SUM_MU, CLV_SUM_Z, CLV_SUM_LOG_LAMBDA, CLV_SUM_LOG_MU,
-  CLV_SUM_LAMBDA2, CLV_SUM_MU2, CLV_SUM_ETA, CLV_SUM_LOG_ETA, CLV_N_SUM_STATS
+  CLV_SUM_LAMBDA2, CLV_SUM_MU2, CLV_SUM_ETA, CLV_SUM_LOG_ETA, CLV_SUM_MU_CAPPED, CLV_SUM_TAU,
+  CLV_N_SUM_STATS
 };
 
 typedef struct clv_config {
@@ -260,6 +267,9 @@ int clv_track_sampler(clv_sampler* s, const double* birth_week, const double* ti
  * utils/analysis_bi_helpers.py:15-27 (post_mean_*) and :75-107 (compute_table4). */
 int clv_level1_summary(int32_t device, const double* level1, int64_t n_draws, int64_t n, int32_t width,
                        double mu_cap, double* out);
+/* The _sampler variant also serves a CLV_SINK_SUMMARY_PCT sampler (no level-1 draws kept): means
+ * from its running sums (pooled over chains), percentiles from its float32 (lambda, mu) store;
+ * mu_cap must then be CLV_SUMMARY_MU_CAP. */
 int clv_level1_summary_sampler(clv_sampler* s, double mu_cap, double* out);
 /* Mean over draws of the total log-likelihood incl. -lgamma(x+1) (analysis_bi_helpers.py:52-72). */
 int clv_chain_total_loglik(int32_t device, const double* level1, int64_t n_draws, int64_t n, int32_t width,

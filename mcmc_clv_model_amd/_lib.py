@@ -19,13 +19,14 @@ except Exception:  # pragma: no cover - torch is optional for the single-GPU pat
 LIB_NAME = "libclvmcmc.so"
 LIB_PATH = os.environ.get("CLV_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 BLOCK = 256
 MAX_K = 9
 MAX_D = 3
 RNG_PHILOX, RNG_REPLAY = 0, 1
-SINK_FULL, SINK_SUMMARY, SINK_NONE = 0, 1, 2
-SUM_STATS = ("lambda", "mu", "z", "log_lambda", "log_mu", "lambda2", "mu2", "eta", "log_eta")
+SINK_FULL, SINK_SUMMARY, SINK_NONE, SINK_SUMMARY_PCT = 0, 1, 2, 3
+SUM_STATS = ("lambda", "mu", "z", "log_lambda", "log_mu", "lambda2", "mu2", "eta", "log_eta", "mu_capped", "tau")
+SUMMARY_MU_CAP = 0.05  # CLV_SUMMARY_MU_CAP: the "mu_capped" sum is of min(mu, 0.05) (analysis_bi_helpers.py:89)
 N_SUM_STATS = len(SUM_STATS)
 TAPE_HYPER = 40
 

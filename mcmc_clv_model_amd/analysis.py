@@ -87,7 +87,13 @@ def draw_future_transactions_rfm_m(cbs: pd.DataFrame, draws: Dict[str, Any], T_s
 
 def level1_summary(draws: Dict[str, Any], mu_cap: float = 0.05, *, device: int = -1) -> pd.DataFrame:
     """Per-customer posterior statistics computed on the GPU: means of lambda, mu, min(mu, mu_cap),
-    z, tau (and eta), and numpy-'linear' 2.5 / 97.5 percentiles of lambda and mu."""
+    z, tau (and eta), and numpy-'linear' 2.5 / 97.5 percentiles of lambda and mu.  A result of
+    ``draw_sink="summary+pct"`` (no level-1 draws) carries them already, formed on the device at
+    the end of the run (``draws["summary"]["level1"]``; mu_cap 0.05 only)."""
+    if draws.get("level_1") is None and isinstance(draws.get("summary"), dict) and "level1" in draws["summary"]:
+        if mu_cap != _lib.SUMMARY_MU_CAP:
+            raise ValueError("a summary run's capped mean of mu uses mu_cap = 0.05")
+        return draws["summary"]["level1"]
     L = _L()
     a = _stacked_level1(draws["level_1"])
     nd, n, w = a.shape

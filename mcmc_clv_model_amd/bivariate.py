@@ -5,7 +5,9 @@ line and return layout (bivariate/mcmc.py:437-504); the sweeps run on the GPU
 (csrc/kernels.hip).  Keyword-only extras:
 
 * ``draw_sink``: "full" (level_1 draws, reference layout), "summary" (per-customer posterior
-  means kept on device; ``level_1`` is None), "none".
+  means kept on device; ``level_1`` is None), "summary+pct" (as "summary", plus Table 4's
+  per-customer 2.5/97.5 percentiles of lambda and mu from a float32 store of the draws:
+  ``out["summary"]["level1"]``, which ``analysis.compute_table4(out)`` uses), "none".
 * ``rng``: "philox" (counter-based, default) or "replay" (test mode: consume variates recorded
   from the reference's numpy Generator, ``replay_tape``).
 * ``device``: HIP device ordinal (-1 = current).

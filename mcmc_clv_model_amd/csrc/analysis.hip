@@ -219,9 +219,38 @@ __global__ void offsets_kernel(int64_t nc, int64_t n_draws, uint32_t* off) {
   if (c <= nc) off[c] = (uint32_t)(c * n_draws);
 }
 
+// CLV_SINK_SUMMARY_PCT: column col (0 lambda, 1 mu) of customers [i0, i0 + nc) from the sampler's
+// float32 store [chain * draw][n] to [customer][chain * draw] (the sort's segments).
+__global__ __launch_bounds__(256) void gather_q_kernel(const float2* q, int64_t n_draws, int64_t n, int col,
+                                                       int64_t i0, int64_t nc, float* seg) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= nc * n_draws) return;
+  const int64_t d = e / nc, c = e - d * nc;  // consecutive lanes: consecutive customers (coalesced reads)
+  const float2 v = q[d * n + i0 + c];
+  seg[c * n_draws + d] = col ? v.y : v.x;
+}
+
+// CLV_SINK_SUMMARY_PCT: per-customer means from the running sums, pooled over chains (chain order).
+__global__ __launch_bounds__(256) void sums_mean_kernel(const double* sums, int n_chains, int64_t n, int64_t n_stored,
+                                                        int D, double* out /*[n][CLV_N_L1_STATS]*/) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int stat[6] = {CLV_SUM_LAMBDA, CLV_SUM_MU, CLV_SUM_MU_CAPPED, CLV_SUM_Z, CLV_SUM_TAU, CLV_SUM_ETA};
+  const int dst[6] = {CLV_L1_MEAN_LAMBDA, CLV_L1_MEAN_MU, CLV_L1_MEAN_MU_CAPPED, CLV_L1_MEAN_Z, CLV_L1_MEAN_TAU,
+                      CLV_L1_MEAN_ETA};
+  const double tot = (double)n_chains * (double)n_stored;
+  for (int k = 0; k < 6; ++k) {
+    double acc = 0.0;
+    for (int c = 0; c < n_chains; ++c) acc += sums[((int64_t)c * CLV_N_SUM_STATS + stat[k]) * n + i];
+    out[i * CLV_N_L1_STATS + dst[k]] = (k == 5 && D != 3) ? 0.0 : acc / tot;
+  }
+}
+
 // numpy.percentile(a, q, method='linear') of a sorted segment (numpy/lib/_function_base_impl.py:
-// virtual index (n-1) q, floor/next neighbours, _lerp with the t >= 0.5 branch).
-__device__ double np_percentile_sorted(const double* a, int64_t n, double q_percent) {
+// virtual index (n-1) q, floor/next neighbours, _lerp with the t >= 0.5 branch); float32 segments
+// (the percentile store) are widened to double before the interpolation, as numpy would on them.
+template <class T>
+__device__ double np_percentile_sorted(const T* a, int64_t n, double q_percent) {
   const double q = q_percent / 100.0;
   const double v = (double)(n - 1) * q;
   int64_t prev, next;
@@ -234,16 +263,17 @@ __device__ double np_percentile_sorted(const double* a, int64_t n, double q_perc
     next = prev + 1;
   }
   const double gamma = v - floor(v);
-  const double lo = a[prev], hi = a[next];
+  const double lo = (double)a[prev], hi = (double)a[next];
   const double diff = hi - lo;
   return gamma >= 0.5 ? hi - diff * (1.0 - gamma) : lo + diff * gamma;
 }
 
-__global__ __launch_bounds__(256) void percentile_kernel(const double* sorted, int64_t nc, int64_t n_draws,
+template <class T>
+__global__ __launch_bounds__(256) void percentile_kernel(const T* sorted, int64_t nc, int64_t n_draws,
                                                          int64_t i0, int col_lo, int col_hi, double* out) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= nc) return;
-  const double* a = sorted + c * n_draws;
+  const T* a = sorted + c * n_draws;
   double* o = out + (i0 + c) * CLV_N_L1_STATS;
   o[col_lo] = np_percentile_sorted(a, n_draws, 2.5);
   o[col_hi] = np_percentile_sorted(a, n_draws, 97.5);
@@ -380,8 +410,56 @@ int summary_dev(const double* l1, int64_t n_draws, int64_t n, int32_t width, dou
       CLV_HIP(rocprim::segmented_radix_sort_keys(btmp.p, tb, (const double*)bin.p, (double*)bsorted.p, (unsigned)ne,
                                                  (unsigned)nc, (const uint32_t*)boff.p, (const uint32_t*)boff.p + 1,
                                                  0, 64, st));
-      hipLaunchKernelGGL(percentile_kernel, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, st,
+      hipLaunchKernelGGL(percentile_kernel<double>, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, st,
                          (const double*)bsorted.p, nc, n_draws, i0, lo_idx[q], hi_idx[q], dout);
+      CLV_HIP(hipGetLastError());
+    }
+  }
+  CLV_HIP(hipMemcpyAsync(out, dout, sizeof(double) * n * CLV_N_L1_STATS, hipMemcpyDeviceToHost, st));
+  CLV_HIP(hipStreamSynchronize(st));
+  return CLV_OK;
+}
+
+// CLV_SINK_SUMMARY_PCT sampler: means from the running sums, exact order statistics of the float32
+// (lambda, mu) store (segmented radix sort on 32-bit keys, customers in batches of <= 2^27 keys).
+int summary_pct_dev(clv_sampler* s, double* out) {
+  const Geometry& g = s->g;
+  const int64_t n = g.n, n_draws = (int64_t)g.n_chains * g.n_draws;
+  hipStream_t st = s->stream;
+  DevBuf bo;
+  CLV_HIP(hipMalloc(&bo.p, sizeof(double) * n * CLV_N_L1_STATS));
+  double* dout = (double*)bo.p;
+  hipLaunchKernelGGL(sums_mean_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, (const double*)s->d_sums,
+                     g.n_chains, n, (int64_t)g.n_draws, g.D, dout);
+  CLV_HIP(hipGetLastError());
+  const int64_t per_batch = std::max<int64_t>(1, std::min<int64_t>(n, (int64_t(1) << 27) / n_draws));
+  DevBuf bin, bsorted, boff, btmp;
+  const size_t keys = (size_t)per_batch * n_draws;
+  CLV_HIP(hipMalloc(&bin.p, sizeof(float) * keys));
+  CLV_HIP(hipMalloc(&bsorted.p, sizeof(float) * keys));
+  CLV_HIP(hipMalloc(&boff.p, sizeof(uint32_t) * (per_batch + 1)));
+  size_t tmp_bytes = 0;
+  CLV_HIP(rocprim::segmented_radix_sort_keys((void*)nullptr, tmp_bytes, (const float*)bin.p, (float*)bsorted.p,
+                                             (unsigned)keys, (unsigned)per_batch, (const uint32_t*)boff.p,
+                                             (const uint32_t*)boff.p + 1, 0, 32, st));
+  CLV_HIP(hipMalloc(&btmp.p, std::max<size_t>(tmp_bytes, 16)));
+  const int lo_idx[2] = {CLV_L1_LAMBDA_P025, CLV_L1_MU_P025};
+  const int hi_idx[2] = {CLV_L1_LAMBDA_P975, CLV_L1_MU_P975};
+  for (int64_t i0 = 0; i0 < n; i0 += per_batch) {
+    const int64_t nc = std::min<int64_t>(per_batch, n - i0);
+    hipLaunchKernelGGL(offsets_kernel, dim3((unsigned)((nc + 256) / 256)), dim3(256), 0, st, nc, n_draws,
+                       (uint32_t*)boff.p);
+    for (int q = 0; q < 2; ++q) {
+      const int64_t ne = nc * n_draws;
+      hipLaunchKernelGGL(gather_q_kernel, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, st,
+                         (const float2*)s->d_qstore, n_draws, n, q, i0, nc, (float*)bin.p);
+      CLV_HIP(hipGetLastError());
+      size_t tb = tmp_bytes;
+      CLV_HIP(rocprim::segmented_radix_sort_keys(btmp.p, tb, (const float*)bin.p, (float*)bsorted.p, (unsigned)ne,
+                                                 (unsigned)nc, (const uint32_t*)boff.p, (const uint32_t*)boff.p + 1,
+                                                 0, 32, st));
+      hipLaunchKernelGGL(percentile_kernel<float>, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, st,
+                         (const float*)bsorted.p, nc, n_draws, i0, lo_idx[q], hi_idx[q], dout);
       CLV_HIP(hipGetLastError());
     }
   }
@@ -493,6 +571,17 @@ int clv_level1_summary(int32_t device, const double* level1, int64_t n_draws, in
 }
 
 int clv_level1_summary_sampler(clv_sampler* s, double mu_cap, double* out) {
+  if (s && !s->d_level1 && s->d_qstore) {  // CLV_SINK_SUMMARY_PCT
+    if (!out) return fail(CLV_EINVAL, "null argument");
+    if (mu_cap != CLV_SUMMARY_MU_CAP) return fail(CLV_EINVAL, "a summary sampler's capped mean uses mu_cap = CLV_SUMMARY_MU_CAP");
+    int64_t stored = 0;
+    if (s->sweeps_done > s->g.burnin) stored = (s->sweeps_done - 1 - s->g.burnin) / s->g.thin + 1;
+    if (std::min<int64_t>(stored, s->g.n_draws) < (int64_t)s->g.n_draws)
+      return fail(CLV_ESTATE, "the run has not stored all of its draws yet");
+    CLV_HIP(hipSetDevice(s->device));
+    CLV_HIP(hipStreamSynchronize(s->stream));
+    return summary_pct_dev(s, out);
+  }
   const double* l1;
   int64_t nd;
   int32_t w;

@@ -56,6 +56,7 @@ SweepArgs sweep_args(clv_sampler* s, int init, int fuse = 0) {
   a.ctrl = s->d_ctrl;
   a.level1 = s->d_level1;
   a.sums = s->d_sums;
+  a.qstore = s->d_qstore;
   a.n_stored = nullptr;
   a.lam_init = s->prior.lam_init;
   a.init = init;
@@ -306,7 +307,7 @@ int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* pri
   if (cfg->burnin < 0 || cfg->mcmc < 0) return fail(CLV_EINVAL, "burnin/mcmc must be >= 0");
   if (cfg->n_chains < 1) return fail(CLV_EINVAL, "n_chains must be >= 1");
   if (cfg->rng_mode != CLV_RNG_PHILOX && cfg->rng_mode != CLV_RNG_REPLAY) return fail(CLV_EINVAL, "bad rng_mode");
-  if (cfg->draw_sink < CLV_SINK_FULL || cfg->draw_sink > CLV_SINK_NONE) return fail(CLV_EINVAL, "bad draw_sink");
+  if (cfg->draw_sink < CLV_SINK_FULL || cfg->draw_sink > CLV_SINK_SUMMARY_PCT) return fail(CLV_EINVAL, "bad draw_sink");
   if (data->n < 0) return fail(CLV_EINVAL, "n must be >= 0");
   if (cfg->n_global > 0xffffffffLL) return fail(CLV_EINVAL, "n_global must fit the 32-bit Philox customer counter");
   if (cfg->n_global < data->n || cfg->n_global < 1) return fail(CLV_EINVAL, "n_global must be >= n >= 0 and > 0");
@@ -429,7 +430,8 @@ int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* pri
     CLV_HIPC(dalloc(&s->d_lam_alt, C * std::max<int64_t>(n, 1)));
     CLV_HIPC(dalloc(&s->d_mu_alt, C * std::max<int64_t>(n, 1)));
     CLV_HIPC(dalloc(&s->d_hyper_alt, C * HS));
-    if (cfg->draw_sink == CLV_SINK_SUMMARY && n > 0) CLV_HIPC(dalloc(&s->d_sums_prev, (size_t)C * CLV_N_SUM_STATS * n));
+    if ((cfg->draw_sink == CLV_SINK_SUMMARY || cfg->draw_sink == CLV_SINK_SUMMARY_PCT) && n > 0)
+      CLV_HIPC(dalloc(&s->d_sums_prev, (size_t)C * CLV_N_SUM_STATS * n));
     CLV_HIPC(hipHostMalloc((void**)&s->h_abort, sizeof(uint32_t), hipHostMallocMapped));
     *s->h_abort = 0;
     CLV_HIPC(hipHostGetDevicePointer((void**)&s->d_h_abort, s->h_abort, 0));
@@ -480,9 +482,19 @@ int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* pri
       CLV_HIPC(hipMemsetAsync(s->d_level1, 0, bytes, s->stream));
     }
   }
-  if (cfg->draw_sink == CLV_SINK_SUMMARY && n > 0) {
+  if ((cfg->draw_sink == CLV_SINK_SUMMARY || cfg->draw_sink == CLV_SINK_SUMMARY_PCT) && n > 0) {
     CLV_HIPC(dalloc(&s->d_sums, (size_t)C * CLV_N_SUM_STATS * n));
     CLV_HIPC(hipMemsetAsync(s->d_sums, 0, sizeof(double) * C * CLV_N_SUM_STATS * n, s->stream));
+  }
+  if (cfg->draw_sink == CLV_SINK_SUMMARY_PCT && n > 0 && g.n_draws > 0) {
+    const size_t nq = (size_t)C * g.n_draws * n;
+    if (hipMalloc((void**)&s->d_qstore, sizeof(float2) * nq) != hipSuccess) {
+      (void)hipGetLastError();
+      s->d_qstore = nullptr;
+      return cleanup_fail(fail(CLV_ENOMEM, "percentile store: " + std::to_string(sizeof(float2) * nq) +
+                                               " bytes of device memory not available"));
+    }
+    CLV_HIPC(hipMemsetAsync(s->d_qstore, 0, sizeof(float2) * nq, s->stream));
   }
   CLV_HIPC(hipMemsetAsync(s->d_block, 0, sizeof(double) * C * bpr * g.stride, s->stream));
   if (bpu > 1) CLV_HIPC(hipMemsetAsync(s->d_unit, 0, sizeof(double) * C * g.units_per_rank * g.stride, s->stream));
@@ -554,7 +566,7 @@ void clv_destroy(clv_sampler* s) {
   if (s->d_unit && s->d_unit != s->d_block) (void)hipFree(s->d_unit);
   if (s->d_hyp2) (void)hipFree(s->d_hyp2);
   for (void* p : {(void*)s->d_lam_alt, (void*)s->d_mu_alt, (void*)s->d_hyper_alt, (void*)s->d_sums_prev,
-                  (void*)s->d_pblock})
+                  (void*)s->d_pblock, (void*)s->d_qstore})
     if (p) (void)hipFree(p);
   if (s->h_abort) (void)hipHostFree(s->h_abort);
   for (void* p : s->ipc_opened) (void)hipIpcCloseMemHandle(p);
@@ -916,7 +928,7 @@ int clv_read_summary(clv_sampler* s, double* sums, int64_t* n_stored) {
     *n_stored = std::min<int64_t>(k, g.n_draws);
   }
   if (sums) {
-    if (!s->d_sums) return fail(CLV_ESTATE, "summaries need draw_sink == CLV_SINK_SUMMARY");
+    if (!s->d_sums) return fail(CLV_ESTATE, "summaries need draw_sink == CLV_SINK_SUMMARY (or _PCT)");
     CLV_HIP(hipMemcpy(sums, s->d_sums, sizeof(double) * g.n_chains * CLV_N_SUM_STATS * g.n, hipMemcpyDeviceToHost));
   }
   return CLV_OK;

@@ -98,6 +98,7 @@ struct clv_sampler {
   double* d_hvar = nullptr;         // [chain][HV] precomputed hyper variates
   unsigned long long* d_stamps = nullptr;  // CLV_STAMPS diagnostic build only
   double *d_level1 = nullptr, *d_level2 = nullptr, *d_loglik = nullptr, *d_sums = nullptr;
+  float2* d_qstore = nullptr;       // CLV_SINK_SUMMARY_PCT: [chain][draw][n] (lambda, mu) float32
   double* d_tape = nullptr;
   double* d_bs = nullptr;  // staging for set_hyper
   int64_t tape_sweeps = 0;

@@ -93,6 +93,7 @@ struct SweepArgs {
   double* hyp2;              // persistent kernel: [2][chain][HS] (beta, Sigma) hand-off slots by sweep parity
   double* level1;            // [chain][n_draws][n][D+2] or null
   double* sums;              // [chain][CLV_N_SUM_STATS][n] or null
+  float2* qstore;            // CLV_SINK_SUMMARY_PCT: [chain][n_draws][n] (lambda, mu) float32, or null
   int64_t* n_stored;         // device counter of stored draws (chain 0 block 0 bumps it)
   double lam_init;
   int init;                  // 1: initialisation pass (bi:367-370), no sweep

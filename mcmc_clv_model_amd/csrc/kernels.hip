@@ -1254,7 +1254,11 @@ __device__ __forceinline__ void cust_store(const Cust<D, K>& u, const CustOut<D>
         sm[CLV_SUM_ETA * g.n] += o.eta;
         sm[CLV_SUM_LOG_ETA * g.n] += log(o.eta);
       }
+      sm[CLV_SUM_MU_CAPPED * g.n] += fmin(o.mu, CLV_SUMMARY_MU_CAP);  // np.clip(mu, None, 0.05)
+      sm[CLV_SUM_TAU * g.n] += u.tau;
     }
+    if (a.qstore)  // one coalesced 8-byte store per lane
+      a.qstore[((int64_t)c * g.n_draws + dr) * g.n + i] = make_float2((float)o.lam, (float)o.mu);
   }
   if (store_state) {
     const int64_t ci = (int64_t)c * g.n + i;

@@ -121,7 +121,9 @@ def resolve_seed(seed: Optional[int]) -> int:
     return seed
 
 
-_SINKS = {"full": _lib.SINK_FULL, "summary": _lib.SINK_SUMMARY, "none": _lib.SINK_NONE}
+# "summary+pct": the summary sums plus a float32 (lambda, mu) store for Table 4's percentiles
+_SINKS = {"full": _lib.SINK_FULL, "summary": _lib.SINK_SUMMARY, "summary+pct": _lib.SINK_SUMMARY_PCT,
+          "none": _lib.SINK_NONE}
 _RNGS = {"philox": _lib.RNG_PHILOX, "replay": _lib.RNG_REPLAY}
 
 
@@ -279,7 +281,7 @@ class HipSampler:
         return l1, l2, ll
 
     def read_summary(self):
-        sums = np.empty((self.chains, _lib.N_SUM_STATS, self.n))
+        sums = np.empty((self.chains, _lib.N_SUM_STATS, self.n))  # also for "summary+pct"
         k = ctypes.c_int64()
         check(self._L.clv_read_summary(self.h, dptr(sums), ctypes.byref(k)))
         return sums, int(k.value)
@@ -315,7 +317,9 @@ class HipSampler:
         return (x, spend) if simulate_spend else x
 
     def level1_summary(self, mu_cap: float = 0.05) -> np.ndarray:
-        """clv_level1_summary_sampler: [n][len(_lib.L1_STATS)] per-customer statistics."""
+        """clv_level1_summary_sampler: [n][len(_lib.L1_STATS)] per-customer statistics (full sink:
+        from the level-1 draws in HBM; "summary+pct": means from the running sums, percentiles from
+        the float32 (lambda, mu) store)."""
         out = np.empty((self.n, len(_lib.L1_STATS)), np.float64)
         check(self._L.clv_level1_summary_sampler(self.h, float(mu_cap), dptr(out)))
         return out
@@ -384,10 +388,16 @@ def fit(p: Problem, *, mcmc: int, burnin: int, thin: int, chains: int, seed, tra
         out = dict(level_1=[l1[c] for c in range(chains)] if l1 is not None else None,
                    level_2=[l2[c] for c in range(chains)],
                    log_likelihood=np.mean(ll.reshape(-1)) if ll.size else np.float64("nan"))
-        if draw_sink == "summary":
+        if draw_sink in ("summary", "summary+pct"):
             sums, k = s.read_summary()
-            names = _lib.SUM_STATS if p.D == 3 else _lib.SUM_STATS[:7]
-            out["summary"] = dict(n_draws=k, **{nm: sums[:, j, :] / max(k, 1) for j, nm in enumerate(names)})
+            names = [nm for nm in _lib.SUM_STATS if p.D == 3 or nm not in ("eta", "log_eta")]
+            out["summary"] = dict(n_draws=k, **{nm: sums[:, _lib.SUM_STATS.index(nm), :] / max(k, 1) for nm in names})
+            if draw_sink == "summary+pct" and k == s.n_draws and k > 0:
+                # per-customer posterior statistics pooled over chains (Table 4's columns)
+                import pandas as pd
+                cols = list(_lib.L1_STATS if p.D == 3 else _lib.L1_STATS[:-1])
+                out["summary"]["level1"] = pd.DataFrame(s.level1_summary(_lib.SUMMARY_MU_CAP)[:, :len(cols)],
+                                                        columns=cols)
         return out
     finally:
         s.close()

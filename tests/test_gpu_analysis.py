@@ -159,3 +159,41 @@ def test_sampler_resident_analysis_equals_host_path():
         birth = np.zeros(len(df))
         times = np.arange(1.0, 40.0)
         assert np.array_equal(s.track(birth, times, seed=1), analysis.posterior_weekly_tracking(draws, birth, times, seed=1))
+
+
+@pytest.mark.parametrize("D", [2, 3])
+def test_summary_pct_sink_matches_full_sink(D):
+    """Verdict r1 #9 (Table 4 where level-1 draws do not fit, c4/c5 scale): the sink does not change
+    the chain (same seed, same trajectory), so a "summary+pct" run must reproduce the full-sink
+    run's per-customer statistics — percentiles bit for bit equal to numpy's 'linear' percentile of
+    the float32-rounded draws (the store's precision) and within 2^-23 relative of the float64
+    draws'; means (pooled over chains from the running sums) within 1e-12 relative of numpy's
+    axis-0 means — and compute_table4 gives the same table."""
+    from mcmc_clv_model_amd import mcmc_draw_parameters, mcmc_draw_parameters_rfm_m
+    from mcmc_clv_model_amd.analysis import compute_table4, level1_summary
+    from tests.helpers import cdnow
+    df = cdnow("abe", 1500)
+    fn, covs = ((mcmc_draw_parameters, ["first_sales_scaled"]) if D == 2 else
+                (mcmc_draw_parameters_rfm_m, ["gender_F", "age_scaled"]))
+    kw = dict(mcmc=301, burnin=40, thin=3, chains=3, seed=11, trace=0)
+    full = fn(df, covs, **kw)
+    pct = fn(df, covs, draw_sink="summary+pct", **kw)
+    assert pct["level_1"] is None
+    assert all(np.array_equal(_bits(a), _bits(b)) for a, b in zip(full["level_2"], pct["level_2"]))
+    l1 = np.concatenate(full["level_1"], axis=0)
+    s = pct["summary"]["level1"]
+    for col, name in [(0, "lambda"), (1, "mu")]:
+        x = l1[:, :, col]
+        x32 = x.astype(np.float32).astype(np.float64)
+        for q, tag in [(2.5, "p025"), (97.5, "p975")]:
+            got = s[f"{name}_{tag}"].to_numpy()
+            assert np.array_equal(_bits(got), _bits(np.percentile(x32, q, axis=0)))
+            np.testing.assert_allclose(got, np.percentile(x, q, axis=0), rtol=2.0 ** -23, atol=0)
+    ref = level1_summary(full)
+    for c in ["mean_lambda", "mean_mu", "mean_mu_capped", "mean_z", "mean_tau"] + (["mean_eta"] if D == 3 else []):
+        np.testing.assert_allclose(s[c].to_numpy(), ref[c].to_numpy(), rtol=1e-12, atol=1e-300)
+    if D == 2:  # Table 4 (bivariate, analysis_bi_helpers.py:75-166): same ranking, same rounded values
+        t_full, t_pct = compute_table4(full), compute_table4(pct)
+        assert list(t_full.index) == list(t_pct.index)
+        num = t_full.drop(index="…").astype(float)
+        np.testing.assert_allclose(t_pct.drop(index="…").astype(float).to_numpy(), num.to_numpy(), rtol=0, atol=1e-4)

@@ -76,12 +76,13 @@ def test_c_abi_rejects_bad_configs():
     from mcmc_clv_model_amd.sampler import build_problem, make_prior
     L = _lib.lib()
     p = build_problem(cdnow("abe", 300), [], 2)
-    base = dict(abi_version=1, D=2, K=1, n_mh_steps=20, burnin=0, mcmc=2, thin=1, n_chains=1, chain_first=0,
+    base = dict(abi_version=_lib.ABI_VERSION, D=2, K=1, n_mh_steps=20, burnin=0, mcmc=2, thin=1, n_chains=1, chain_first=0,
                 rng_mode=0, draw_sink=0, device=-1, seed=1, n_global=300, shard_begin=0, world_size=1, rank=0,
                 blocks_per_rank=0, blocks_per_unit=0, stream=0)
     data = _lib.ClvData(n=300, x=p.x.ctypes.data, t_x=p.t_x.ctypes.data, T_cal=p.T_cal.ctypes.data)
     pr = make_prior(p)
-    for bad in (dict(D=4), dict(K=10), dict(thin=0), dict(n_chains=0), dict(abi_version=2), dict(blocks_per_unit=3),
+    for bad in (dict(D=4), dict(K=10), dict(thin=0), dict(n_chains=0), dict(abi_version=_lib.ABI_VERSION + 1),
+                dict(draw_sink=4), dict(blocks_per_unit=3),
                 dict(world_size=2, rank=0, blocks_per_rank=0), dict(rng_mode=1, world_size=2, blocks_per_rank=2),
                 dict(n_global=299), dict(shard_begin=256)):
         cfg = _lib.ClvConfig(**dict(base, **bad))
