@@ -237,6 +237,28 @@ int clv_debug_mh_step(int64_t n, const int32_t* x, const uint8_t* z, const doubl
  * workgroups (+1 level-2 workgroup each) on n_cu CUs — out[linear workgroup] = chain << 16 | block. */
 int clv_debug_wg_map(int32_t n_chains, int32_t nb, int32_t n_cu, int32_t* out);
 
+/* ---- In-process multi-device runs (SURVEY.md §8b devices=, §8e) ----
+ * A group drives the n shards of one problem from one host thread: shards[r] = the sampler of rank
+ * r of a world of n (clv_create with world_size n, blocks_per_rank / blocks_per_unit of the shard
+ * plan, each on its own device or sharing one), all at the same sweep.  Per sweep the shards
+ * exchange their unit partials (the all-gather of bi:243-255's statistics) either
+ *   CLV_EXCHANGE_P2P:  every shard's persistent grid fits at once (on shared devices: together) and
+ *                      distinct devices have peer access — clv_p2p_connect by device pointers, one
+ *                      persistent launch per shard and call, all in flight before any is awaited;
+ *   CLV_EXCHANGE_COPY: per sweep the sweep kernels, device-to-device copies of each shard's unit
+ *                      partials into every shard's gathered buffer (stream-ordered by events), and
+ *                      every shard's level-2 draw.
+ * CLV_EXCHANGE_AUTO picks P2P where possible.  Results are bitwise those of the unsharded run.  A
+ * P2P call that times out on any shard is undone on the others and redone by copies (kept).
+ * clv_group_run is synchronous; the bivariate initial draw (bi:393 of sweep 1) is its first
+ * exchange.  The group does not own the shards (destroy the group first). */
+enum { CLV_EXCHANGE_AUTO = 0, CLV_EXCHANGE_P2P = 1, CLV_EXCHANGE_COPY = 2 };
+typedef struct clv_group clv_group;
+int clv_group_create(clv_sampler* const* shards, int32_t n, int32_t exchange, clv_group** out);
+int clv_group_run(clv_group* g, int64_t n_sweeps);
+int32_t clv_group_exchange(const clv_group* g);
+void clv_group_destroy(clv_group* g);
+
 /* ---- Posterior analysis on device ----
  * Inputs are level-1 draws [n_draws][n][width] in the reference's layout, chains stacked
  * (np.vstack of draws["level_1"]); width 4 = (lambda, mu, tau, z), 5 = (+ eta).  The plain

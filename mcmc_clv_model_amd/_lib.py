@@ -25,6 +25,7 @@ MAX_K = 9
 MAX_D = 3
 RNG_PHILOX, RNG_REPLAY = 0, 1
 SINK_FULL, SINK_SUMMARY, SINK_NONE, SINK_SUMMARY_PCT = 0, 1, 2, 3
+EXCHANGE_AUTO, EXCHANGE_P2P, EXCHANGE_COPY = 0, 1, 2
 SUM_STATS = ("lambda", "mu", "z", "log_lambda", "log_mu", "lambda2", "mu2", "eta", "log_eta", "mu_capped", "tau")
 SUMMARY_MU_CAP = 0.05  # CLV_SUMMARY_MU_CAP: the "mu_capped" sum is of min(mu, 0.05) (analysis_bi_helpers.py:89)
 N_SUM_STATS = len(SUM_STATS)
@@ -117,6 +118,10 @@ def lib() -> ctypes.CDLL:
         "clv_debug_mh_step": (c_int32, [c_int64, POINTER(c_int32), POINTER(c_uint8), dp, dp, dp, dp, dp,
                                         POINTER(c_float), dp, POINTER(c_float), dp]),
         "clv_debug_wg_map": (c_int32, [c_int32, c_int32, c_int32, POINTER(c_int32)]),
+        "clv_group_create": (c_int32, [POINTER(sp), c_int32, c_int32, POINTER(sp)]),
+        "clv_group_run": (c_int32, [sp, c_int64]),
+        "clv_group_exchange": (c_int32, [sp]),
+        "clv_group_destroy": (None, [sp]),
         "clv_predict": (c_int32, [c_int32, dp, c_int64, c_int64, c_int32, dp, c_double, c_uint64, c_int32, c_double,
                                   POINTER(c_int64), dp]),
         "clv_predict_sampler": (c_int32, [sp, c_double, c_uint64, c_int32, c_double, POINTER(c_int64), dp]),

@@ -11,6 +11,11 @@ line and return layout (bivariate/mcmc.py:437-504); the sweeps run on the GPU
 * ``rng``: "philox" (counter-based, default) or "replay" (test mode: consume variates recorded
   from the reference's numpy Generator, ``replay_tape``).
 * ``device``: HIP device ordinal (-1 = current).
+* ``devices``: several device ordinals — the run is spread over them from this process
+  (``shard="chains"``: chain groups, one host thread each; ``"customers"``: every chain's customers
+  split into shards exchanging the level-2 statistics each sweep by peer stores or device copies,
+  ``exchange`` = "auto" | "p2p" | "copy"; ``"auto"``: chains when they divide evenly), with the
+  single-device run's output bit for bit (sampler.fit_multi, csrc/group.hip).
 """
 from __future__ import annotations
 
@@ -26,7 +31,8 @@ def mcmc_draw_parameters(cal_cbs, covariates: Optional[Sequence[str]] = None, mc
                          burnin: int = 500, thin: int = 50, chains: int = 2, seed: Optional[int] = None,
                          trace: int = 100, n_mh_steps: int = 20, *, draw_sink: str = "full",
                          rng: str = "philox", device: int = -1, replay_tape=None,
-                         replay_sweeps: Optional[int] = None):
+                         replay_sweeps: Optional[int] = None, devices: Optional[Sequence[int]] = None,
+                         shard: str = "auto", exchange: str = "auto"):
     """Run the Abe (2009) Gibbs/MH sampler on calibration CBS (bivariate/mcmc.py:437).
 
     Returns dict(level_1=[(n_draws, N, 4) per chain: lambda, mu, tau, z],
@@ -43,4 +49,5 @@ def mcmc_draw_parameters(cal_cbs, covariates: Optional[Sequence[str]] = None, mc
     p = build_problem(cal_cbs, covariates, D=2)
     return fit(p, mcmc=mcmc, burnin=burnin, thin=thin, chains=chains, seed=seed, trace=trace,
                n_mh_steps=n_mh_steps, draw_sink=draw_sink, rng=rng, device=device,
-               replay_tape=replay_tape, replay_sweeps=replay_sweeps)
+               replay_tape=replay_tape, replay_sweeps=replay_sweeps, devices=devices, shard=shard,
+               exchange=exchange)

@@ -740,12 +740,16 @@ int clv_note_sweeps(clv_sampler* s, int64_t n) {
   return CLV_OK;
 }
 
-namespace {
-// Persistent path: one launch of persist_kernel for all n sweeps (see kernels.hip).
-int run_persistent(clv_sampler* s, int64_t n_sweeps) {
-  if (n_sweeps == 0) return CLV_OK;
+}  // extern "C"
+
+// Persistent path: one launch of persist_kernel for all n sweeps (see kernels.hip), in two halves
+// so that a group of shards in one process (group.hip) can have every shard's launch in flight
+// before waiting for any.
+int clv::persist_launch(clv_sampler* s, int64_t n_sweeps) {
   const Geometry& g = s->g;
   s->last_persist_n = 0;
+  s->inflight_n = 0;
+  if (n_sweeps == 0) return CLV_OK;
   if (s->slots_dirty) {  // a completed launch leaves every hand-off slot empty; else fill them
     // every hand-off slot empty (all-ones bytes: the sentinel NaN)
     CLV_HIP(hipMemsetAsync(s->d_hyp2, 0xFF, sizeof(double) * 2 * g.n_chains * HS, s->stream));
@@ -766,9 +770,9 @@ int run_persistent(clv_sampler* s, int64_t n_sweeps) {
     s->ev_sweeps[s->ev_used] = n_sweeps;
   }
   CLV_HIP(launch_persist(a, s->sweeps_done + 1, n_sweeps, s->stream, e0, e1));
-  // wait for the launch: its end event (timing: the dispatch's own end timestamp; else one
-  // recorded behind it).  Timed launches are harvested later (clv_kernel_time or a full slot set).
-  hipEvent_t done = e1;
+  // the launch's end event (timing: the dispatch's own end timestamp; else one recorded behind
+  // it).  Timed launches are harvested later (clv_kernel_time or a full slot set).
+  s->inflight_done = e1;
   if (s->timing) {
     if (++s->ev_used == TIMING_EVENTS) {
       int rc = harvest_timing(s);
@@ -777,8 +781,18 @@ int run_persistent(clv_sampler* s, int64_t n_sweeps) {
   } else if (s->sync_mode != 0) {
     if (!s->done_ev) CLV_HIP(hipEventCreateWithFlags(&s->done_ev, hipEventDisableTiming));
     CLV_HIP(hipEventRecord(s->done_ev, s->stream));
-    done = s->done_ev;
+    s->inflight_done = s->done_ev;
   }
+  s->inflight_n = n_sweeps;
+  return CLV_OK;
+}
+
+int clv::persist_wait(clv_sampler* s) {
+  const int64_t n_sweeps = s->inflight_n;
+  if (n_sweeps == 0) return CLV_OK;
+  s->inflight_n = 0;
+  const Geometry& g = s->g;
+  const hipEvent_t done = s->inflight_done;
   if (s->sync_mode == 0 || !done) {
     CLV_HIP(hipStreamSynchronize(s->stream));
   } else if (s->sync_mode == 1) {
@@ -796,6 +810,7 @@ int run_persistent(clv_sampler* s, int64_t n_sweeps) {
     Ctrl c{};
     c.cur = s->sweeps_done;
     CLV_HIP(hipMemcpy(s->d_ctrl, &c, sizeof(Ctrl), hipMemcpyHostToDevice));
+    const size_t sums_bytes = sizeof(double) * (size_t)g.n_chains * CLV_N_SUM_STATS * g.n;
     if (s->d_sums_prev) CLV_HIP(hipMemcpy(s->d_sums, s->d_sums_prev, sums_bytes, hipMemcpyDeviceToDevice));
     s->slots_dirty = true;
     if (g.world_size > 1) s->p2p_ready = false;  // mail slots are in an unknown state now
@@ -816,7 +831,16 @@ int run_persistent(clv_sampler* s, int64_t n_sweeps) {
   s->last_persist_n = n_sweeps;
   return CLV_OK;
 }
+
+namespace {
+int run_persistent(clv_sampler* s, int64_t n_sweeps) {
+  int rc = persist_launch(s, n_sweeps);
+  if (rc) return rc;
+  return persist_wait(s);
+}
 }  // namespace
+
+extern "C" {
 
 int clv_run(clv_sampler* s, int64_t n_sweeps) {
   if (!s) return fail(CLV_EINVAL, "null sampler");

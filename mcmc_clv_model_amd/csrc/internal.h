@@ -13,6 +13,11 @@ namespace clv {
 // Records msg as the calling thread's clv_last_error() and returns code.
 int fail(int code, const std::string& msg);
 
+// Persistent path in two halves (capi.hip): enqueue one launch of n sweeps; wait for it and adopt
+// its carried state (or restore the state it started from, if a wait in it timed out).
+int persist_launch(clv_sampler* s, int64_t n_sweeps);
+int persist_wait(clv_sampler* s);
+
 template <class T>
 hipError_t dalloc(T** p, size_t count) {
   *p = nullptr;
@@ -113,6 +118,8 @@ struct clv_sampler {
   // 1 poll hipEventQuery on the launch's end event, 2 hipEventSynchronize on it
   int sync_mode = 1;
   hipEvent_t done_ev = nullptr;     // recorded after each untimed persistent launch (timing: e1)
+  int64_t inflight_n = 0;           // sweeps of the persistent launch in flight (persist_launch)
+  hipEvent_t inflight_done = nullptr;  // its end event (null: wait with hipStreamSynchronize)
   int pre_variates = 1;             // CLV_PRE_VARIATES (read at create)
 
   bool timing = false;

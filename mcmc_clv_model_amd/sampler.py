@@ -22,6 +22,8 @@ import numpy as np
 from . import _lib
 from ._lib import check, dptr
 
+BLOCK_SIZE = _lib.BLOCK
+
 
 @dataclass
 class Problem:
@@ -346,13 +348,55 @@ class HipSampler:
         return dict(sweep_ms=a.value, sweep_launches=na.value, hyper_ms=b.value, hyper_launches=nb.value)
 
 
+_EXCHANGES = {"auto": _lib.EXCHANGE_AUTO, "p2p": _lib.EXCHANGE_P2P, "copy": _lib.EXCHANGE_COPY}
+
+
+class HipGroup:
+    """clv_group (include/clvmcmc.h): the shards of one problem — HipSampler handles of ranks
+    0..n-1 of a world of n, on their own devices or sharing one — run from this one thread, with
+    the unit partials exchanged per sweep by peer stores (persistent kernels, "p2p") or
+    stream-ordered device-to-device copies ("copy").  Does not own the shards."""
+
+    def __init__(self, shards: Sequence[HipSampler], exchange: str = "auto"):
+        if exchange not in _EXCHANGES:
+            raise ValueError(f"exchange must be one of {sorted(_EXCHANGES)}")
+        L = _lib.lib()
+        arr = (ctypes.c_void_p * len(shards))(*[sh.h.value for sh in shards])
+        h = ctypes.c_void_p()
+        check(L.clv_group_create(arr, len(shards), _EXCHANGES[exchange], ctypes.byref(h)))
+        self.h, self._L, self.shards = h, L, list(shards)
+
+    def run(self, n_sweeps: int) -> None:
+        check(self._L.clv_group_run(self.h, int(n_sweeps)))
+
+    @property
+    def exchange(self) -> str:
+        return {_lib.EXCHANGE_P2P: "p2p", _lib.EXCHANGE_COPY: "copy"}[int(self._L.clv_group_exchange(self.h))]
+
+    def close(self) -> None:
+        if getattr(self, "h", None):
+            self._L.clv_group_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def trace_marks(total: int, trace: int) -> List[int]:
+    """Steps at which the reference prints its trace line (bi:383-384: ``step % trace == 0``)."""
+    return [m for m in range(trace, total + 1, trace)] if trace else []
+
+
 def run_with_trace(s: HipSampler, total: int, trace: int, n_chains_label: int = 1, chain_offset: int = 0) -> None:
     """Run ``total`` sweeps, printing the reference's trace line (bi:383-384) for every chain at
     every step that is a multiple of ``trace``, in the reference's order: its chains run one after
     another (bi:484), so all lines of chain 1 come before any line of chain 2.  Here the chains
     advance together: chain 1's lines are printed live (as the reference does, before the step
     runs), the other chains' lines — identical text — once all sweeps are done."""
-    marks = [m for m in range(trace, total + 1, trace)] if trace else []
+    marks = trace_marks(total, trace)
     done = 0
     for m in marks:
         if m - 1 > done:  # the reference prints at the start of step m
@@ -366,16 +410,46 @@ def run_with_trace(s: HipSampler, total: int, trace: int, n_chains_label: int = 
             print(f"chain {chain_offset + ch + 1} | step {m}/{total}")
 
 
+def _assemble(D: int, chains: int, l1, l2, ll, sums, k: int, n_draws: int, draw_sink: str, level1_stats) -> dict:
+    """The reference's output layout (bi:499-504) from [chain]-leading arrays: level_1 / level_2
+    lists with one array per chain, the marginal log-likelihood = mean over all chains' per-draw
+    means, and (summary sinks) the per-customer running means."""
+    out = dict(level_1=[l1[c] for c in range(chains)] if l1 is not None else None,
+               level_2=[l2[c] for c in range(chains)],
+               log_likelihood=np.mean(ll.reshape(-1)) if ll.size else np.float64("nan"))
+    if draw_sink in ("summary", "summary+pct"):
+        names = [nm for nm in _lib.SUM_STATS if D == 3 or nm not in ("eta", "log_eta")]
+        out["summary"] = dict(n_draws=k, **{nm: sums[:, _lib.SUM_STATS.index(nm), :] / max(k, 1) for nm in names})
+        if draw_sink == "summary+pct" and k == n_draws and k > 0:
+            # per-customer posterior statistics pooled over chains (Table 4's columns)
+            import pandas as pd
+            cols = list(_lib.L1_STATS if D == 3 else _lib.L1_STATS[:-1])
+            out["summary"]["level1"] = pd.DataFrame(level1_stats()[:, :len(cols)], columns=cols)
+    return out
+
+
 def fit(p: Problem, *, mcmc: int, burnin: int, thin: int, chains: int, seed, trace: int, n_mh_steps: int,
         draw_sink: str = "full", rng: str = "philox", device: int = -1, replay_tape=None,
-        replay_sweeps: Optional[int] = None) -> dict:
+        replay_sweeps: Optional[int] = None, devices: Optional[Sequence[int]] = None, shard: str = "auto",
+        exchange: str = "auto") -> dict:
     """Run all chains of one problem in one batched launch sequence and return the reference's
-    output layout (bi:499-504): level_1 / level_2 lists with one array per chain, and the
-    marginal log-likelihood = mean over all chains' per-draw means."""
+    output layout (bi:499-504).  ``devices`` (two or more): the run is spread over those devices
+    in this process (:func:`fit_multi`)."""
     if chains < 1:
         raise ValueError("chains must be >= 1")
     if thin < 1:
         raise ValueError("thin must be >= 1")
+    if devices is not None:
+        devices = [int(d) for d in devices]
+        if not devices:
+            raise ValueError("devices must name at least one device")
+        if len(devices) > 1:
+            if rng != "philox":
+                raise ValueError("devices= runs need rng='philox' (the replay tape is a single-device test mode)")
+            return fit_multi(p, mcmc=mcmc, burnin=burnin, thin=thin, chains=chains, seed=seed, trace=trace,
+                             n_mh_steps=n_mh_steps, draw_sink=draw_sink, devices=devices, shard=shard,
+                             exchange=exchange)
+        device = devices[0]
     s = HipSampler(p, mcmc=mcmc, burnin=burnin, thin=thin, chains=chains, seed=resolve_seed(seed),
                    n_mh_steps=n_mh_steps, draw_sink=draw_sink, rng=rng, device=device)
     try:
@@ -385,19 +459,116 @@ def fit(p: Problem, *, mcmc: int, burnin: int, thin: int, chains: int, seed, tra
             s.set_replay_tape(replay_tape, replay_sweeps)
         run_with_trace(s, burnin + mcmc, trace, n_chains_label=chains)
         l1, l2, ll = s.read_draws(level1=draw_sink == "full")
-        out = dict(level_1=[l1[c] for c in range(chains)] if l1 is not None else None,
-                   level_2=[l2[c] for c in range(chains)],
-                   log_likelihood=np.mean(ll.reshape(-1)) if ll.size else np.float64("nan"))
-        if draw_sink in ("summary", "summary+pct"):
-            sums, k = s.read_summary()
-            names = [nm for nm in _lib.SUM_STATS if p.D == 3 or nm not in ("eta", "log_eta")]
-            out["summary"] = dict(n_draws=k, **{nm: sums[:, _lib.SUM_STATS.index(nm), :] / max(k, 1) for nm in names})
-            if draw_sink == "summary+pct" and k == s.n_draws and k > 0:
-                # per-customer posterior statistics pooled over chains (Table 4's columns)
-                import pandas as pd
-                cols = list(_lib.L1_STATS if p.D == 3 else _lib.L1_STATS[:-1])
-                out["summary"]["level1"] = pd.DataFrame(s.level1_summary(_lib.SUMMARY_MU_CAP)[:, :len(cols)],
-                                                        columns=cols)
-        return out
+        sums, k = s.read_summary() if draw_sink in ("summary", "summary+pct") else (None, 0)
+        return _assemble(p.D, chains, l1, l2, ll, sums, k, s.n_draws, draw_sink,
+                         lambda: s.level1_summary(_lib.SUMMARY_MU_CAP))
     finally:
         s.close()
+
+
+def fit_multi(p: Problem, *, mcmc: int, burnin: int, thin: int, chains: int, seed, trace: int, n_mh_steps: int,
+              draw_sink: str, devices: Sequence[int], shard: str = "auto", exchange: str = "auto") -> dict:
+    """One run over several devices of this process (SURVEY §8b ``devices=``), same output as the
+    single-device run, bit for bit:
+
+    * ``shard="chains"``: the chains in contiguous groups, one group per device, each group run from
+      its own host thread (the reference runs its chains one after another, bi:481-488 — they are
+      independent; Philox draws depend on (seed, chain, customer, sweep) only);
+    * ``shard="customers"``: every chain's customers split into contiguous shards (the shard plan
+      of :mod:`distributed`), one per device, exchanging the level-2 statistics every sweep
+      (:class:`HipGroup`: peer stores from persistent kernels where every grid fits at once, else
+      device-to-device copies; ``exchange`` forces one);
+    * ``"auto"``: chains when they divide evenly over the devices (and the sink is not
+      "summary+pct", whose percentiles pool all chains), else customers."""
+    import threading
+    n_dev = len(devices)
+    if shard not in ("auto", "chains", "customers"):
+        raise ValueError("shard must be 'auto', 'chains' or 'customers'")
+    if shard == "auto":
+        shard = "chains" if (chains % n_dev == 0 and draw_sink != "summary+pct") else "customers"
+    if shard == "chains" and draw_sink == "summary+pct":
+        raise ValueError("draw_sink='summary+pct' pools every chain's draws: use shard='customers'")
+    seed = resolve_seed(seed)
+    total = burnin + mcmc
+    kw = dict(mcmc=mcmc, burnin=burnin, thin=thin, seed=seed, n_mh_steps=n_mh_steps, draw_sink=draw_sink)
+    if shard == "chains":
+        n_grp = min(n_dev, chains)
+        sizes = [chains // n_grp + (1 if g < chains % n_grp else 0) for g in range(n_grp)]
+        firsts = [sum(sizes[:g]) for g in range(n_grp)]
+        samplers = []
+        try:
+            for g in range(n_grp):
+                samplers.append(HipSampler(p, chains=sizes[g], chain_first=firsts[g], device=devices[g], **kw))
+            errs = []
+
+            def go(g):
+                try:
+                    if g == 0:  # chain 1's trace lines live, as the reference prints them
+                        run_with_trace(samplers[0], total, trace, n_chains_label=1)
+                    else:
+                        samplers[g].run(total)
+                except Exception as e:  # noqa: BLE001 - re-raised below
+                    errs.append(e)
+            th = [threading.Thread(target=go, args=(g,)) for g in range(n_grp)]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+            if errs:
+                raise errs[0]
+            for ch in range(1, chains):
+                for m in trace_marks(total, trace):
+                    print(f"chain {ch + 1} | step {m}/{total}")
+            reads = [sm.read_draws(level1=draw_sink == "full") for sm in samplers]
+            l1 = np.concatenate([r[0] for r in reads], axis=0) if draw_sink == "full" else None
+            l2 = np.concatenate([r[1] for r in reads], axis=0)
+            ll = np.concatenate([r[2] for r in reads], axis=0)
+            sums, k = (None, 0)
+            if draw_sink == "summary":
+                rs = [sm.read_summary() for sm in samplers]
+                sums, k = np.concatenate([r[0] for r in rs], axis=0), rs[0][1]
+            return _assemble(p.D, chains, l1, l2, ll, sums, k, samplers[0].n_draws, draw_sink, None)
+        finally:
+            for sm in samplers:
+                sm.close()
+    # customers
+    from . import distributed as Dm
+    plan = Dm.plan(p.N, n_dev)
+    prior = make_prior(p, p.N)
+    shards = []
+    group = None
+    try:
+        for r in range(n_dev):
+            b, e = plan.shard(r)
+            shards.append(HipSampler(Dm.slice_problem(p, b, e), chains=chains, device=devices[r], n_global=p.N,
+                                     shard_begin=r * plan.blocks_per_rank * BLOCK_SIZE, world_size=n_dev, rank=r,
+                                     blocks_per_rank=plan.blocks_per_rank, blocks_per_unit=plan.blocks_per_unit,
+                                     prior=prior, **kw))
+        group = HipGroup(shards, exchange)
+        done = 0
+        for m in trace_marks(total, trace):  # as run_with_trace: chain 1 live, the others after
+            if m - 1 > done:
+                group.run(m - 1 - done)
+                done = m - 1
+            print(f"chain 1 | step {m}/{total}")
+        if total > done:
+            group.run(total - done)
+        for ch in range(1, chains):
+            for m in trace_marks(total, trace):
+                print(f"chain {ch + 1} | step {m}/{total}")
+        reads = [sh.read_draws(level1=draw_sink == "full") for sh in shards]
+        l1 = np.concatenate([r[0] for r in reads], axis=2) if draw_sink == "full" else None
+        l2, ll = reads[0][1], reads[0][2]  # every shard drew the same level 2 (same bits)
+        sums, k = (None, 0)
+        if draw_sink in ("summary", "summary+pct"):
+            rs = [sh.read_summary() for sh in shards]
+            sums, k = np.concatenate([r[0] for r in rs], axis=2), rs[0][1]
+        out = _assemble(p.D, chains, l1, l2, ll, sums, k, shards[0].n_draws, draw_sink,
+                        lambda: np.concatenate([sh.level1_summary(_lib.SUMMARY_MU_CAP) for sh in shards], axis=0))
+        out["exchange"] = group.exchange
+        return out
+    finally:
+        if group is not None:
+            group.close()
+        for sh in shards:
+            sh.close()

@@ -18,7 +18,8 @@ def mcmc_draw_parameters_rfm_m(cal_cbs, covariates: Optional[Sequence[str]] = No
                                burnin: int = 500, thin: int = 50, chains: int = 2,
                                seed: Optional[int] = None, trace: int = 100, n_mh_steps: int = 20, *,
                                draw_sink: str = "full", rng: str = "philox", device: int = -1,
-                               replay_tape=None, replay_sweeps: Optional[int] = None):
+                               replay_tape=None, replay_sweeps: Optional[int] = None,
+                               devices: Optional[Sequence[int]] = None, shard: str = "auto", exchange: str = "auto"):
     """3-dimensional HB Pareto/NBD + spend sampler (trivariate/mcmc.py:580).
 
     Returns {"level_1": [(n_draws, N, 5) per chain: lambda, mu, tau, z, eta],
@@ -29,6 +30,7 @@ def mcmc_draw_parameters_rfm_m(cal_cbs, covariates: Optional[Sequence[str]] = No
     p = build_problem(cal_cbs, covariates, D=3)
     out = fit(p, mcmc=mcmc, burnin=burnin, thin=thin, chains=chains, seed=seed, trace=trace,
               n_mh_steps=n_mh_steps, draw_sink=draw_sink, rng=rng, device=device,
-              replay_tape=replay_tape, replay_sweeps=replay_sweeps)
+              replay_tape=replay_tape, replay_sweeps=replay_sweeps, devices=devices, shard=shard,
+               exchange=exchange)
     out["log_likelihood"] = float(out["log_likelihood"])  # tri:652 returns a Python float
     return out
