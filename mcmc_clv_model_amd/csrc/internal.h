@@ -121,6 +121,8 @@ struct clv_sampler {
   int64_t inflight_n = 0;           // sweeps of the persistent launch in flight (persist_launch)
   hipEvent_t inflight_done = nullptr;  // its end event (null: wait with hipStreamSynchronize)
   int pre_variates = 1;             // CLV_PRE_VARIATES (read at create)
+  bool timing_record = true;        // timed persistent launches bracketed by hipEventRecord
+                                    // (CLV_TIMING_RECORD=0: the dispatch's own timestamps)
 
   bool timing = false;
   std::vector<hipEvent_t> ev;  // 4 per slot: sweep start/end, hyper start/end
