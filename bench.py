@@ -48,10 +48,16 @@ def algorithmic_bytes(D: int, K: int, stored_frac: float, draw_sink: str) -> flo
     """HBM bytes one (chain, customer) moves per sweep in the sweep kernel:
     read x (4) + t_x, T (16) + K-1 covariates (8 each) + log_s (D=3: 8) + lambda, mu (16);
     write lambda, mu (16); per stored sweep (share `stored_frac`): the level-1 draw 8(D+2)
-    (full sink) or the read-modify-write of 7 (D=2) / 9 (D=3) running sums (summary sink)."""
+    (full sink) or the read-modify-write of 9 (D=2) / 11 (D=3) running sums (summary sinks; plus
+    the float32 (lambda, mu) pair, 8, for "summary+pct")."""
     rd = 4 + 16 + 8 * (K - 1) + (8 if D == 3 else 0) + 16
     wr = 16
-    per_store = 8.0 * (D + 2) if draw_sink == "full" else (16.0 * (7 if D == 2 else 9) if draw_sink == "summary" else 0.0)
+    if draw_sink == "full":
+        per_store = 8.0 * (D + 2)
+    elif draw_sink in ("summary", "summary+pct"):
+        per_store = 16.0 * (9 if D == 2 else 11) + (8.0 if draw_sink == "summary+pct" else 0.0)
+    else:
+        per_store = 0.0
     return rd + wr + per_store * stored_frac
 
 
@@ -246,7 +252,10 @@ def measure_config(name: str, world: int, rank: int, local_rank: int, dist, step
                 ms_per_step=dt / steps * 1e3, draw_sink=sink,
                 hbm_frac=round(bpu * value / 1e9 / (world * HBM_PEAK_GBS), 5), bytes_per_unit=round(bpu, 2),
                 path=("persistent kernel" if persistent else "launch-per-sweep sweep kernel") +
-                     ("" if world == 1 else f", exchange {exch}" + (f" ({note})" if note else "")))
+                     ("" if world == 1 else
+                      (", unit partials stored into every rank's mail over xGMI by the kernel (no host collective)"
+                       if exch == "p2p" else ", RCCL all-gather + level-2 kernel per sweep") +
+                      (f" ({note})" if note else "")))
 
 
 def main():
@@ -330,8 +339,8 @@ def main():
     sync()
     if dist:
         dist.barrier()
-    # persistent kernel: the timed launch itself carries the HIP start/stop events (the dispatch's
-    # own timestamps via hipExtLaunchKernelGGL on the sampler's stream — no extra packets)
+    # persistent kernel: the timed launch itself is bracketed by HIP start/stop events recorded on
+    # the sampler's stream (the launch's stream), inside the timed region
     live = timing and persistent
     if live:
         kern.set_timing(True)

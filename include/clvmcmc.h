@@ -156,8 +156,13 @@ int clv_launch_info(const clv_sampler* s, int64_t* out);
  * own mail holds all ranks' units, and sums them in the same global unit order as clv_hyper — so
  * results are bitwise those of clv_sweep/clv_hyper with an all-gather (and of world size 1).
  * Replaces, per sweep, the all-gather of bi:243-255's statistics.
- *   clv_p2p_info:    out[4] = (capable 0/1, connected 0/1, mail bytes, mail device pointer);
- *                    capable = every workgroup of the persistent grid fits at once on this GPU.
+ *   clv_p2p_info:    out[5] = (capable 0/1, connected 0/1, mail bytes, mail device pointer,
+ *                    persistent 0/1); persistent = every workgroup of the persistent grid fits at
+ *                    once on this GPU.  Otherwise (any shard size) clv_run launches the sweep
+ *                    kernel once per sweep and its fused level-2 tail exchanges the same way: the
+ *                    chain's unit-last workgroups store this rank's unit partials into every rank's
+ *                    mail, the chain's last one waits for all ranks' units in its own mail, sums
+ *                    them in global order and draws — no host collective, no separate launches.
  *   clv_p2p_export:  this rank's mail buffer as a hipIpcMemHandle (CLV_IPC_HANDLE_BYTES bytes).
  *   clv_p2p_connect: every rank's mail: handles = [world][CLV_IPC_HANDLE_BYTES] (opened with
  *                    hipIpcOpenMemHandle; this rank's entry ignored) or ptrs = [world] device

@@ -417,16 +417,22 @@ int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* pri
     if (persist_occupancy(g.D, g.K, true, &s->persist_bpc) == hipSuccess &&
         hipGetDeviceProperties(&prop, s->device) == hipSuccess)
       s->n_cu = prop.multiProcessorCount;
-    if ((int64_t)s->persist_bpc * s->n_cu >= (int64_t)(nb_local + 1) * C) {
+    const char* env = std::getenv("CLV_PERSISTENT");  // "0": the fused exchange below instead
+    if ((!env || std::string(env) != "0") && (int64_t)s->persist_bpc * s->n_cu >= (int64_t)(nb_local + 1) * C)
       s->p2p_capable = true;
-      const int64_t nm = 2LL * g.world_size * C * g.stride * g.units_per_rank;
-      CLV_HIPC(dalloc(&s->d_mail, nm));
-      CLV_HIPC(hipMemsetAsync(s->d_mail, 0xFF, sizeof(double) * nm, s->stream));  // every slot empty
-      CLV_HIPC(dalloc(&s->d_peers, g.world_size));
-    }
   }
-  if (s->persistent || s->p2p_capable) {
-    CLV_HIPC(dalloc(&s->d_pblock, (size_t)C * nb_local * g.stride));
+  // Any other shard: the sweep kernel's fused level-2 tail exchanges through the same mail (one
+  // launch per sweep, no host collective; n_units_global <= 2 CLV_BLOCK as its readers assume)
+  if (!s->replay && cfg->world_size > 1 && cfg->world_size <= MAX_WORLD && g.n_units_global <= 2 * BLOCK)
+    s->fx_capable = true;
+  if (s->p2p_capable || s->fx_capable) {
+    const int64_t nm = 2LL * g.world_size * C * g.stride * g.units_per_rank;
+    CLV_HIPC(dalloc(&s->d_mail, nm));
+    CLV_HIPC(hipMemsetAsync(s->d_mail, 0xFF, sizeof(double) * nm, s->stream));  // every slot empty
+    CLV_HIPC(dalloc(&s->d_peers, g.world_size));
+  }
+  if (s->persistent || s->p2p_capable || s->fx_capable) {  // (fused exchange: the snapshot buffers)
+    CLV_HIPC(dalloc(&s->d_pblock, (size_t)C * std::max(nb_local, 1) * g.stride));
     CLV_HIPC(dalloc(&s->d_lam_alt, C * std::max<int64_t>(n, 1)));
     CLV_HIPC(dalloc(&s->d_mu_alt, C * std::max<int64_t>(n, 1)));
     CLV_HIPC(dalloc(&s->d_hyper_alt, C * HS));
@@ -670,7 +676,8 @@ int clv_launch_info(const clv_sampler* s, int64_t* out) {
 
 int clv_p2p_info(const clv_sampler* s, int64_t* out) {
   if (!s || !out) return fail(CLV_EINVAL, "null argument");
-  out[0] = s->p2p_capable ? 1 : 0;
+  out[0] = (s->p2p_capable || s->fx_capable) ? 1 : 0;
+  out[4] = s->p2p_capable ? 1 : 0;
   out[1] = s->p2p_ready ? 1 : 0;
   out[2] = s->d_mail ? (int64_t)sizeof(double) * 2 * s->g.world_size * s->g.n_chains * s->g.stride * s->g.units_per_rank : 0;
   out[3] = (int64_t)(uintptr_t)s->d_mail;
@@ -679,7 +686,7 @@ int clv_p2p_info(const clv_sampler* s, int64_t* out) {
 
 int clv_p2p_export(clv_sampler* s, void* handle) {
   if (!s || !handle) return fail(CLV_EINVAL, "null argument");
-  if (!s->p2p_capable) return fail(CLV_ESTATE, "no peer exchange for this geometry (grid does not fit at once)");
+  if (!s->p2p_capable && !s->fx_capable) return fail(CLV_ESTATE, "no peer exchange for this sampler (world size 1 or replay mode)");
   CLV_HIP(hipSetDevice(s->device));
   hipIpcMemHandle_t h;
   CLV_HIP(hipIpcGetMemHandle(&h, s->d_mail));
@@ -689,7 +696,7 @@ int clv_p2p_export(clv_sampler* s, void* handle) {
 
 int clv_p2p_connect(clv_sampler* s, const void* handles, const uint64_t* ptrs) {
   if (!s || (!handles && !ptrs)) return fail(CLV_EINVAL, "null argument");
-  if (!s->p2p_capable) return fail(CLV_ESTATE, "no peer exchange for this geometry (grid does not fit at once)");
+  if (!s->p2p_capable && !s->fx_capable) return fail(CLV_ESTATE, "no peer exchange for this sampler (world size 1 or replay mode)");
   CLV_HIP(hipSetDevice(s->device));
   CLV_HIP(hipStreamSynchronize(s->stream));
   if (s->p2p_ready || !s->ipc_opened.empty()) {  // reconnect (after a failed step): drop the old mappings
@@ -848,29 +855,11 @@ int run_persistent(clv_sampler* s, int64_t n_sweeps) {
   if (rc) return rc;
   return persist_wait(s);
 }
-}  // namespace
 
-extern "C" {
-
-int clv_run(clv_sampler* s, int64_t n_sweeps) {
-  if (!s) return fail(CLV_EINVAL, "null sampler");
-  if (s->g.world_size != 1) {
-    if (!s->p2p_ready) return fail(CLV_ESTATE, "sharded clv_run needs clv_p2p_connect; else use clv_sweep/clv_hyper");
-    if (s->pending_init_hyper) return fail(CLV_ESTATE, "bivariate: call clv_hyper once before the first sweep");
-    if (n_sweeps < 0) return fail(CLV_EINVAL, "n_sweeps < 0");
-    CLV_HIP(hipSetDevice(s->device));
-    return run_persistent(s, n_sweeps);
-  }
-  if (n_sweeps < 0) return fail(CLV_EINVAL, "n_sweeps < 0");
-  CLV_HIP(hipSetDevice(s->device));
-  int rc = check_replay_range(s, n_sweeps);
-  if (rc) return rc;
-  if (s->pending_init_hyper) {
-    rc = enqueue_hyper(s, nullptr, 1, nullptr, nullptr);
-    if (rc) return rc;
-    s->pending_init_hyper = false;
-  }
-  if (s->persistent) return run_persistent(s, n_sweeps);
+// n launches of the fused sweep kernel (world size 1, or sharded with the fused peer exchange):
+// hipGraph chunks, or (timing) one event pair per launch.  Not waited for.
+int enqueue_fused_sweeps(clv_sampler* s, int64_t n_sweeps) {
+  int rc = CLV_OK;
   int64_t left = n_sweeps;
   if (s->timing) {
     rc = ensure_events(s);
@@ -887,25 +876,91 @@ int clv_run(clv_sampler* s, int64_t n_sweeps) {
         if (rc) return rc;
       }
     }
-    rc = harvest_timing(s);
+    return harvest_timing(s);
+  }
+  if (left >= GRAPH_CHUNK) {
+    rc = build_graph(s, GRAPH_CHUNK);
     if (rc) return rc;
-  } else {
-    if (left >= GRAPH_CHUNK) {
-      rc = build_graph(s, GRAPH_CHUNK);
-      if (rc) return rc;
-      while (left >= GRAPH_CHUNK) {
-        CLV_HIP(hipGraphLaunch(s->graph_exec, s->stream));
-        s->sweeps_done += GRAPH_CHUNK;
-        left -= GRAPH_CHUNK;
-      }
-    }
-    while (left > 0) {
-      rc = enqueue_fused(s, nullptr, nullptr);
-      if (rc) return rc;
-      s->sweeps_done++;
-      left--;
+    while (left >= GRAPH_CHUNK) {
+      CLV_HIP(hipGraphLaunch(s->graph_exec, s->stream));
+      s->sweeps_done += GRAPH_CHUNK;
+      left -= GRAPH_CHUNK;
     }
   }
+  while (left > 0) {
+    rc = enqueue_fused(s, nullptr, nullptr);
+    if (rc) return rc;
+    s->sweeps_done++;
+    left--;
+  }
+  return CLV_OK;
+}
+
+// World size > 1 without a resident grid: n launches of the sweep kernel whose fused tail
+// exchanges unit partials through the peers' mail (kernels.hip sweep_body, FX).  The state before
+// the call is kept in the persistent path's *_alt buffers, so that a call in which a wait times out
+// (a peer not running; the call's later launches then return at once) leaves it unchanged, and a
+// completed call can be undone by clv_rollback (a step that failed on another rank).
+int run_fused_exchange(clv_sampler* s, int64_t n_sweeps) {
+  s->last_persist_n = 0;
+  if (n_sweeps == 0) return CLV_OK;
+  const Geometry& g = s->g;
+  const size_t nl = sizeof(double) * (size_t)g.n_chains * std::max<int64_t>(g.n, 1);
+  const size_t sums_bytes = sizeof(double) * (size_t)g.n_chains * CLV_N_SUM_STATS * g.n;
+  CLV_HIP(hipMemcpyAsync(s->d_lam_alt, s->d_lam, nl, hipMemcpyDeviceToDevice, s->stream));
+  CLV_HIP(hipMemcpyAsync(s->d_mu_alt, s->d_mu, nl, hipMemcpyDeviceToDevice, s->stream));
+  CLV_HIP(hipMemcpyAsync(s->d_hyper_alt, s->d_hyper, sizeof(double) * g.n_chains * HS, hipMemcpyDeviceToDevice,
+                         s->stream));
+  if (s->d_sums_prev) CLV_HIP(hipMemcpyAsync(s->d_sums_prev, s->d_sums, sums_bytes, hipMemcpyDeviceToDevice, s->stream));
+  const int64_t before = s->sweeps_done;
+  const int rc = enqueue_fused_sweeps(s, n_sweeps);
+  CLV_HIP(hipStreamSynchronize(s->stream));
+  const bool aborted = __atomic_load_n(s->h_abort, __ATOMIC_ACQUIRE) != 0;
+  if (rc == CLV_OK && !aborted) {
+    s->last_persist_n = n_sweeps;
+    return CLV_OK;
+  }
+  // back to the state before the call (copies: a captured graph keeps the buffer addresses)
+  CLV_HIP(hipMemcpy(s->d_lam, s->d_lam_alt, nl, hipMemcpyDeviceToDevice));
+  CLV_HIP(hipMemcpy(s->d_mu, s->d_mu_alt, nl, hipMemcpyDeviceToDevice));
+  CLV_HIP(hipMemcpy(s->d_hyper, s->d_hyper_alt, sizeof(double) * g.n_chains * HS, hipMemcpyDeviceToDevice));
+  if (s->d_sums_prev) CLV_HIP(hipMemcpy(s->d_sums, s->d_sums_prev, sums_bytes, hipMemcpyDeviceToDevice));
+  *s->h_abort = 0;
+  s->sweeps_done = before;
+  Ctrl c{};
+  c.cur = before;
+  CLV_HIP(hipMemcpy(s->d_ctrl, &c, sizeof(Ctrl), hipMemcpyHostToDevice));
+  CLV_HIP(hipMemset(s->d_arrive, 0, sizeof(uint32_t) * (g.n_chains + (int64_t)g.n_chains * g.units_per_rank)));
+  s->p2p_ready = false;  // mail slots in an unknown state: clv_p2p_connect refills them
+  if (rc) return rc;
+  return fail(CLV_EHIP, "fused peer exchange: a wait timed out (a peer rank not running?); state unchanged");
+}
+}  // namespace
+
+extern "C" {
+
+int clv_run(clv_sampler* s, int64_t n_sweeps) {
+  if (!s) return fail(CLV_EINVAL, "null sampler");
+  if (s->g.world_size != 1) {
+    if (!s->p2p_ready) return fail(CLV_ESTATE, "sharded clv_run needs clv_p2p_connect; else use clv_sweep/clv_hyper");
+    if (s->pending_init_hyper) return fail(CLV_ESTATE, "bivariate: call clv_hyper once before the first sweep");
+    if (n_sweeps < 0) return fail(CLV_EINVAL, "n_sweeps < 0");
+    CLV_HIP(hipSetDevice(s->device));
+    if (s->p2p_capable) return run_persistent(s, n_sweeps);
+    return run_fused_exchange(s, n_sweeps);
+  }
+  if (n_sweeps < 0) return fail(CLV_EINVAL, "n_sweeps < 0");
+  CLV_HIP(hipSetDevice(s->device));
+  int rc = check_replay_range(s, n_sweeps);
+  if (rc) return rc;
+  if (s->pending_init_hyper) {
+    rc = enqueue_hyper(s, nullptr, 1, nullptr, nullptr);
+    if (rc) return rc;
+    s->pending_init_hyper = false;
+  }
+  if (s->persistent) return run_persistent(s, n_sweeps);
+  rc = enqueue_fused_sweeps(s, n_sweeps);
+  if (rc) return rc;
   CLV_HIP(hipStreamSynchronize(s->stream));
   return CLV_OK;
 }

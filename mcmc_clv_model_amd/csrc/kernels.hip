@@ -792,17 +792,15 @@ __device__ double chi2_draw(uint32_t k0, uint32_t k1, uint32_t sweep, int idx, d
 // (fused path).  `units`: [world][chain][stride][units_per_rank] unit partials (the gathered
 // buffer; at world size 1 this rank's unit partials, or its block partials when a unit is one
 // block), summed in global unit order — so every path and GPU count is bitwise identical.
-template <int D, int K, bool REPLAY, int NS, int NT>
-__device__ void hyper_body(const HyperArgs& a, int c, int64_t s, int mode, const double* units,
-                           double (*red)[NS], double* tot, double* var_iw, double* var_chi, double* var_noise,
-                           L2Scratch* l2) {
+// Level-2 draw, part 1: stage the prior and this draw's variates (independent of the statistics,
+// so their loads overlap the reduction's).
+template <int D, int K, bool REPLAY>
+__device__ __forceinline__ void hyper_variates(const HyperArgs& a, int c, int64_t s, double* var_iw, double* var_chi,
+                                               double* var_noise, L2Scratch* l2) {
   constexpr int NTRIL = D * (D - 1) / 2;
-  const Geometry& g = a.g;
   const int tid = threadIdx.x;
   const int64_t hs = (D == 2) ? s + 1 : s;  // sweep the drawn (beta, Sigma) belongs to
-
   stage_prior(a.V, l2);  // published by block_reduce's barriers
-  // 1. variates first: independent of the statistics, so their loads overlap the reduction's
   if constexpr (REPLAY) {
     const double* tv = a.r.tape + ((int64_t)c * a.r.tape_sweeps + (hs - 1)) * a.r.tape_sweep_stride +
                        (a.r.tape_sweep_stride - TAPE_HYPER);
@@ -825,12 +823,17 @@ __device__ void hyper_body(const HyperArgs& a, int c, int64_t s, int mode, const
       var_chi[q] = chi2_draw(k0, k1, (uint32_t)hs, q, a.nu_n - D + 1 + q);
     }
   }
-  // 2. fixed-order reduction over all units of all shards (independent of world size).  Unit
-  // partials are read with sc1 loads: in the fused path other CUs wrote them during this launch.
-  double acc[NS];
+}
+
+// Part 2: this lane's share of the fixed-order sum over all units of all shards (independent of
+// world size): lane u sums units u, u + NT, ... in order.  Unit partials are read with sc1 loads:
+// in the fused path other CUs wrote them during this launch.
+template <int NS, int NT>
+__device__ __forceinline__ void hyper_sum_units(const HyperArgs& a, int c, const double* units, double (&acc)[NS]) {
+  const Geometry& g = a.g;
 #pragma unroll
   for (int j = 0; j < NS; ++j) acc[j] = 0.0;
-  for (int64_t u = tid; u < g.n_units_global; u += NT) {
+  for (int64_t u = threadIdx.x; u < g.n_units_global; u += NT) {
     const int64_t r = u / g.units_per_rank;
     const int64_t lu = u - r * g.units_per_rank;
     const double* p = units + (r * g.n_chains + c) * g.stride * (int64_t)g.units_per_rank + lu;
@@ -838,9 +841,18 @@ __device__ void hyper_body(const HyperArgs& a, int c, int64_t s, int mode, const
     for (int j = 0; j < NS; ++j)  // lanes read consecutive units: coalesced
       acc[j] += __hip_atomic_load(p + (int64_t)j * g.units_per_rank, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+}
+
+// Part 3: the workgroup reduction of the lanes' sums, the algebra and the outputs.
+template <int D, int K, bool REPLAY, int NS, int NT>
+__device__ void hyper_finish(const HyperArgs& a, int c, int64_t s, int mode, double (&acc)[NS], double (*red)[NS],
+                             double* tot, double* var_iw, double* var_chi, double* var_noise, L2Scratch* l2) {
+  const Geometry& g = a.g;
+  const int tid = threadIdx.x;
+  const int64_t hs = (D == 2) ? s + 1 : s;
   block_reduce<NS, NT>(acc, red, tot);  // its barriers also publish the variates written to LDS above
 
-  // 3. algebra (element-parallel phases + one-lane core) and outputs
+  // algebra (element-parallel phases + one-lane core) and outputs
   if (tid == 0) CLV_STAMP(a.stamps, s, 6, false);
   L2Scratch* sc = l2;
   level2_draw<D, K>(tot, var_iw, var_chi, var_noise, REPLAY, sc);
@@ -878,6 +890,23 @@ __device__ void hyper_body(const HyperArgs& a, int c, int64_t s, int mode, const
   }
 }
 
+// Level-2 draw of chain c after sweep s (mode 0), or the bivariate initial draw (mode 1):
+// fixed-order sum of all unit partials, variates, algebra, hyper state, level-2 record and
+// log-likelihood, then the sweep-counter arrival.  Executed by one 256-thread workgroup: the
+// standalone hyper_kernel (sharded path) or the last-arriving sweep workgroup of the chain
+// (fused path).  `units`: [world][chain][stride][units_per_rank] unit partials (the gathered
+// buffer; at world size 1 this rank's unit partials, or its block partials when a unit is one
+// block), summed in global unit order — so every path and GPU count is bitwise identical.
+template <int D, int K, bool REPLAY, int NS, int NT>
+__device__ void hyper_body(const HyperArgs& a, int c, int64_t s, int mode, const double* units,
+                           double (*red)[NS], double* tot, double* var_iw, double* var_chi, double* var_noise,
+                           L2Scratch* l2) {
+  hyper_variates<D, K, REPLAY>(a, c, s, var_iw, var_chi, var_noise, l2);
+  double acc[NS];
+  hyper_sum_units<NS, NT>(a, c, units, acc);
+  hyper_finish<D, K, REPLAY, NS, NT>(a, c, s, mode, acc, red, tot, var_iw, var_chi, var_noise, l2);
+}
+
 template <int D, int K, bool REPLAY>
 __global__ __launch_bounds__(256) void hyper_kernel(HyperArgs a) {
   constexpr int NS = K * D + D * (D + 1) / 2 + 1;
@@ -888,6 +917,40 @@ __global__ __launch_bounds__(256) void hyper_kernel(HyperArgs a) {
   const int64_t done = __hip_atomic_load(&a.ctrl->cur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int64_t s = a.mode == 1 ? 0 : done + 1;  // sweep whose statistics are reduced here
   hyper_body<D, K, REPLAY, NS, 256>(a, blockIdx.x, s, a.mode, a.units, red, tot, var_iw, var_chi, var_noise, &l2);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Hand-off helpers (fused peer exchange, persistent kernel)
+// ---------------------------------------------------------------------------------------------
+constexpr long long SLOT_EMPTY = -1ll;              // all-ones bit pattern: a NaN no arithmetic yields
+
+__device__ __forceinline__ double ld_wt(const double* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_wt(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// System scope for the peer exchange: other GPUs write this rank's mail buffer over xGMI.
+__device__ __forceinline__ double ld_sys(const double* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_sys(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ bool slot_full(double v) { return __double_as_longlong(v) != SLOT_EMPTY; }
+__device__ __forceinline__ double slot_empty() { return __longlong_as_double(SLOT_EMPTY); }
+
+// Bounded wait bookkeeping (uniform): true when this wave must give up.  The abort flag is read
+// every 16th poll only, so a poll iteration costs one memory round trip, not two.
+__device__ __forceinline__ bool wait_expired(const SweepArgs& a, uint64_t t0, uint32_t poll) {
+  if ((poll & 15u) == 15u && __hip_atomic_load(&a.ctrl_rw->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+    return true;
+  if (__builtin_amdgcn_s_memrealtime() - t0 > a.wait_ticks) {
+    __hip_atomic_store(&a.ctrl_rw->abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (a.abort_host) __hip_atomic_store(a.abort_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return true;
+  }
+  return false;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1269,7 +1332,12 @@ __device__ __forceinline__ void cust_store(const Cust<D, K>& u, const CustOut<D>
 
 static_assert(BLOCK == EXP_TAB_N, "the sweep kernel stages the exp table with one entry per lane");
 
-template <int D, int K, bool REPLAY>
+// FX: the fused peer exchange (world size > 1 after clv_p2p_connect) compiled in — every Philox
+// instance; it runs only when the launch is sharded.
+#ifndef CLV_FX
+#define CLV_FX 1  // 0: A/B builds without the fused peer exchange
+#endif
+template <int D, int K, bool REPLAY, bool FX = !REPLAY && CLV_FX>
 __device__ __forceinline__ void sweep_body(const SweepArgs& a) {
   constexpr int NT = BLOCK;
   constexpr int NXY = K * D;
@@ -1286,6 +1354,12 @@ __device__ __forceinline__ void sweep_body(const SweepArgs& a) {
   const Geometry& g = a.g;
   const int c = blockIdx.y;
   const int b = blockIdx.x;
+  if constexpr (FX) {  // a wait of an earlier launch of this call timed out: the call fails, and
+                       // its remaining launches return at once (the host restores the state)
+    if (a.fuse && g.world_size > 1 &&
+        __hip_atomic_load(&a.ctrl_rw->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      return;
+  }
   // The customer's loads go out first, so that their latency, the exp table's and the sweep
   // index's overlap (one memory round trip before compute instead of several).
   Cust<D, K> cu;
@@ -1423,6 +1497,16 @@ __device__ __forceinline__ void sweep_body(const SweepArgs& a) {
     __syncthreads();
     const int bpu = g.blocks_per_unit;
     const double* units = a.blockpart;  // a unit is one block
+    // fused peer exchange (world size > 1, clv_p2p_connect): every unit partial goes straight into
+    // every rank's mail, [parity][rank][chain][unit][stat], system-scope write-through stores (the
+    // value is its own arrival flag); the chain's last unit on this rank then waits in its own mail
+    const bool fx = FX && g.world_size > 1;
+    const int64_t mail_rank = (int64_t)g.n_chains * g.units_per_rank * NS;
+    const int64_t mail_off = ((int64_t)(s & 1) * g.world_size + a.rank) * mail_rank + (int64_t)c * g.units_per_rank * NS;
+    if (fx && bpu == 1 && threadIdx.x < NS) {
+      const double v = tot[threadIdx.x];
+      for (int q = 0; q < g.world_size; ++q) st_sys(a.peers[q] + mail_off + (int64_t)b * NS + threadIdx.x, v);
+    }
     if (bpu > 1) {
       const int u = b / bpu;
       const int nbu = min(bpu, g.nb_local - u * bpu);  // blocks of this unit in the launch
@@ -1448,12 +1532,18 @@ __device__ __forceinline__ void sweep_body(const SweepArgs& a) {
           for (int q = 0; q < 8; ++q) t += v[q];
         }
         for (; bb < bpu; ++bb) t += __hip_atomic_load(p + bb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(a.unitpart + ((int64_t)c * g.stride + threadIdx.x) * g.units_per_rank + u, t,
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (fx) {
+          for (int q = 0; q < g.world_size; ++q) st_sys(a.peers[q] + mail_off + (int64_t)u * NS + threadIdx.x, t);
+        } else {
+          __hip_atomic_store(a.unitpart + ((int64_t)c * g.stride + threadIdx.x) * g.units_per_rank + u, t,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
       }
+      units = a.unitpart;
+    }
+    if (bpu > 1 || fx) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      units = a.unitpart;
     }
     if (threadIdx.x == 0) {
       CLV_STAMP(a.stamps, s, 1, false);
@@ -1470,7 +1560,60 @@ __device__ __forceinline__ void sweep_body(const SweepArgs& a) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only
     if (s_last) {
       if (threadIdx.x == 0) CLV_STAMP(a.stamps, s, 2, false);
-      hyper_body<D, K, REPLAY, NS, NT>(a.h, c, s, 0, units, red, tot, var_iw, var_chi, var_noise, &l2);
+      if (!fx) {
+        hyper_body<D, K, REPLAY, NS, NT>(a.h, c, s, 0, units, red, tot, var_iw, var_chi, var_noise, &l2);
+      } else {
+        hyper_variates<D, K, REPLAY>(a.h, c, s, var_iw, var_chi, var_noise, &l2);
+        // every rank's units of sweep s from this rank's mail: lane u reads units u, u + NT
+        // (n_units_global <= 2 NT) and sums them in that order — hyper_sum_units' order, so the
+        // result is the all-gather path's bit for bit; then it empties its slots for sweep s + 2
+        const int64_t u0 = threadIdx.x, u1 = threadIdx.x + NT;
+        const bool h0 = u0 < g.n_units_global, h1 = u1 < g.n_units_global;
+        const double* mb = a.mail + (int64_t)(s & 1) * g.world_size * mail_rank + (int64_t)c * g.units_per_rank * NS;
+        double* p0 = (double*)mb + (u0 / g.units_per_rank) * mail_rank + (u0 % g.units_per_rank) * NS;
+        double* p1 = (double*)mb + (u1 / g.units_per_rank) * mail_rank + (u1 % g.units_per_rank) * NS;
+        const double* q0 = h0 ? p0 : mb;
+        const double* q1 = h1 ? p1 : mb;
+        double v0[NS], v1[NS];
+        __shared__ uint32_t s_fx_abort;
+        if (threadIdx.x == 0) s_fx_abort = 0;
+        __syncthreads();
+        {
+          const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+          for (uint32_t poll = 0;; ++poll) {
+            bool ok = true;
+#pragma unroll
+            for (int j = 0; j < NS; ++j) {
+              v0[j] = ld_sys(q0 + j);
+              v1[j] = ld_sys(q1 + j);
+            }
+#pragma unroll
+            for (int j = 0; j < NS; ++j) ok = ok & (!h0 | slot_full(v0[j])) & (!h1 | slot_full(v1[j]));
+            if (__all(ok)) break;
+            if (wait_expired(a, t0, poll)) {
+              s_fx_abort = 1;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+          }
+        }
+        __syncthreads();
+        if (!s_fx_abort) {
+          double acc[NS];
+#pragma unroll
+          for (int j = 0; j < NS; ++j) {
+            acc[j] = 0.0;
+            if (h0) acc[j] += v0[j];
+            if (h1) acc[j] += v1[j];
+          }
+#pragma unroll
+          for (int j = 0; j < NS; ++j) {
+            if (h0) st_sys(p0 + j, slot_empty());
+            if (h1) st_sys(p1 + j, slot_empty());
+          }
+          hyper_finish<D, K, REPLAY, NS, NT>(a.h, c, s, 0, acc, red, tot, var_iw, var_chi, var_noise, &l2);
+        }
+      }
       if (threadIdx.x == 0) CLV_STAMP(a.stamps, s, 3, false);
     }
   }
@@ -1510,37 +1653,6 @@ __global__ __launch_bounds__(BLOCK, 4) void sweep_kernel_occ4(SweepArgs a) {
 // written to the *_out buffers, which the host adopts only when no wave aborted: an aborted launch
 // leaves the state it started from untouched.
 // ---------------------------------------------------------------------------------------------
-constexpr long long SLOT_EMPTY = -1ll;              // all-ones bit pattern: a NaN no arithmetic yields
-
-__device__ __forceinline__ double ld_wt(const double* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_wt(double* p, double v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// System scope for the peer exchange: other GPUs write this rank's mail buffer over xGMI.
-__device__ __forceinline__ double ld_sys(const double* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ void st_sys(double* p, double v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ bool slot_full(double v) { return __double_as_longlong(v) != SLOT_EMPTY; }
-__device__ __forceinline__ double slot_empty() { return __longlong_as_double(SLOT_EMPTY); }
-
-// Bounded wait bookkeeping (uniform): true when this wave must give up.  The abort flag is read
-// every 16th poll only, so a poll iteration costs one memory round trip, not two.
-__device__ __forceinline__ bool wait_expired(const SweepArgs& a, uint64_t t0, uint32_t poll) {
-  if ((poll & 15u) == 15u && __hip_atomic_load(&a.ctrl_rw->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-    return true;
-  if (__builtin_amdgcn_s_memrealtime() - t0 > a.wait_ticks) {
-    __hip_atomic_store(&a.ctrl_rw->abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (a.abort_host) __hip_atomic_store(a.abort_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    return true;
-  }
-  return false;
-}
-
 // The chain's level-2 workgroup of persist_kernel (one per chain, grid column nb_local).
 // register arrays (block/unit partials of the chain) do not raise the customer path's pressure.
 template <int D, int K, bool P2P>

@@ -179,8 +179,8 @@ class ShardedSampler:
         capable = self._all_ok(self.s.p2p_info()["capable"])
         if not capable:
             if required:
-                raise _lib.ClvError("p2p exchange: the persistent grid does not fit at once on every rank")
-            self.p2p_note = "not capable (grid does not fit at once on every rank)"
+                raise _lib.ClvError("p2p exchange: not available on every rank")
+            self.p2p_note = "not capable on every rank"
             return
         handles = [None] * self.world
         dist.all_gather_object(handles, self.s.p2p_export(), group=self.group)
@@ -278,9 +278,10 @@ class ShardedSampler:
         torch.cuda.synchronize()
 
     def launch_info(self) -> dict:
-        """clv_launch_info, with ``persistent`` = this rank runs whole steps in one launch (p2p)."""
+        """clv_launch_info, with ``persistent`` = this rank runs whole steps in one launch (p2p with
+        a resident grid; else p2p runs one fused sweep launch per sweep)."""
         info = self.s.launch_info()
-        info["persistent"] = self.exchange == "p2p"
+        info["persistent"] = self.exchange == "p2p" and self.s.p2p_info()["persistent"]
         return info
 
     def set_timing(self, enable: bool) -> None:

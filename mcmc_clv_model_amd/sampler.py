@@ -239,9 +239,12 @@ class HipSampler:
     IPC_HANDLE_BYTES = 64
 
     def p2p_info(self) -> dict:
-        out = (ctypes.c_int64 * 4)()
+        """clv_p2p_info: peer exchange possible / connected, the mail buffer, and whether clv_run
+        runs it in one persistent launch (else one fused sweep launch per sweep)."""
+        out = (ctypes.c_int64 * 5)()
         check(self._L.clv_p2p_info(self.h, out))
-        return dict(capable=bool(out[0]), connected=bool(out[1]), mail_bytes=int(out[2]), mail_ptr=int(out[3]))
+        return dict(capable=bool(out[0]), connected=bool(out[1]), mail_bytes=int(out[2]), mail_ptr=int(out[3]),
+                    persistent=bool(out[4]))
 
     def p2p_export(self) -> bytes:
         """This rank's mail buffer as a hipIpcMemHandle (bytes) for the other ranks."""

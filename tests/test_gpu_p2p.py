@@ -118,6 +118,87 @@ def test_p2p_persistent_bitwise_equals_unsharded(D, covs, n, world, sink):
             sh.close()
 
 
+@pytest.mark.parametrize("D,covs,n,world,sink,persistent_off", [
+    (2, ["first_sales_scaled"], 23570, 2, "full", True),
+    (3, ["gender_F", "age_scaled"], 23570, 3, "summary", True),
+    # too large for a resident grid per shard: the fused exchange by itself, blocks_per_unit 4
+    (2, ["c1", "c2", "c3", "c4"], 300000, 2, "summary", False)])
+def test_fused_exchange_bitwise_equals_unsharded(monkeypatch, D, covs, n, world, sink, persistent_off):
+    """World size > 1 without the persistent grid (verdict r1 #7: the c4/c5-size shards exchanged
+    without an RCCL all-gather and a separate level-2 launch per sweep): clv_run launches the sweep
+    kernel once per sweep (hipGraph chunks of 64) and its fused tail stores this rank's unit
+    partials into every rank's mail, waits for all ranks' units in its own and draws — bitwise the
+    unsharded run (state, draws / summaries, level-2 records, log-likelihood)."""
+    import torch
+    from mcmc_clv_model_amd import distributed as Dm
+    from mcmc_clv_model_amd.data import synthetic_cbs
+    from mcmc_clv_model_amd.sampler import HipSampler, build_problem, make_prior
+    if persistent_off:
+        monkeypatch.setenv("CLV_PERSISTENT", "0")
+    df = synthetic_cbs(n, len(covs) + 1, D, seed=n) if covs[0] == "c1" else cdnow("full", n)
+    p = build_problem(df, covs, D)
+    kw = dict(mcmc=40, burnin=50, thin=3, chains=2 if n < 100000 else 1, seed=2024, draw_sink=sink)
+    chunks = (1, 5, 70, 3)
+    sweeps = sum(chunks)
+    kw["mcmc"] = sweeps - kw["burnin"]
+    ref, ref_sums, ref_l1, ref_l2, ref_ll = _ref_run(p, sweeps, kw)
+    plan = Dm.plan(p.N, world)
+    prior = make_prior(p, p.N)
+    shards = []
+    for r in range(world):
+        b, e = plan.shard(r)
+        shards.append(HipSampler(Dm.slice_problem(p, b, e), n_global=p.N, shard_begin=r * plan.blocks_per_rank * 256,
+                                 world_size=world, rank=r, blocks_per_rank=plan.blocks_per_rank,
+                                 blocks_per_unit=plan.blocks_per_unit, prior=prior, **kw))
+    try:
+        info = [sh.p2p_info() for sh in shards]
+        assert all(i["capable"] and not i["persistent"] for i in info), info
+        assert all(not sh.launch_info()["persistent"] for sh in shards)
+        if D == 2:
+            nd = shards[0].partials()[1]
+            gathered = torch.zeros(nd * world, dtype=torch.float64, device="cuda")
+            for r, sh in enumerate(shards):
+                sh.copy_partials(gathered.data_ptr() + r * nd * 8)
+                sh.synchronize()
+            for sh in shards:
+                sh.hyper(gathered.data_ptr())
+                sh.synchronize()
+        ptrs = [i["mail_ptr"] for i in info]
+        for sh in shards:
+            sh.p2p_connect(ptrs=ptrs)
+        for n_run in chunks:
+            errs = []
+
+            def go(sh):
+                try:
+                    sh.run(n_run)
+                except Exception as e:  # noqa: BLE001
+                    errs.append(e)
+
+            th = [threading.Thread(target=go, args=(sh,)) for sh in shards]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join(timeout=120)
+            assert not any(t.is_alive() for t in th)
+            assert not errs, errs
+        for r, sh in enumerate(shards):
+            b, e = plan.shard(r)
+            assert sh.sweeps_done == sweeps
+            lam, mu, beta, sigma = sh.get_state()
+            assert np.array_equal(bits(lam), bits(ref[0][:, b:e])) and np.array_equal(bits(mu), bits(ref[1][:, b:e]))
+            assert np.array_equal(bits(beta), bits(ref[2])) and np.array_equal(bits(sigma), bits(ref[3]))
+            l1, l2, ll = sh.read_draws(level1=sink == "full")
+            assert np.array_equal(bits(l2), bits(ref_l2)) and np.array_equal(bits(ll), bits(ref_ll))
+            if sink == "full":
+                assert np.array_equal(bits(l1), bits(ref_l1[:, :, b:e]))
+            else:
+                assert np.array_equal(bits(sh.read_summary()[0]), bits(ref_sums[:, :, b:e]))
+    finally:
+        for sh in shards:
+            sh.close()
+
+
 WORKER = r"""
 import json, os, sys
 sys.path.insert(0, os.environ["CLV_ROOT"])
@@ -151,17 +232,18 @@ dist.destroy_process_group()
 """
 
 
-@pytest.mark.parametrize("D", [2, 3])
-def test_p2p_two_processes_ipc(D):
+@pytest.mark.parametrize("D,persistent", [(2, "1"), (3, "1"), (2, "0")])
+def test_p2p_two_processes_ipc(D, persistent):
     """Two processes (one rank each) on the one GPU: hipIpcMemHandle exchange, verification
-    against the all-gather path, then 17 sweeps in two steps — bitwise equal to the unsharded run."""
+    against the all-gather path, then 17 sweeps in two steps — bitwise equal to the unsharded run
+    (persistent = "0": through the fused exchange)."""
     with socket.socket() as so:
         so.bind(("127.0.0.1", 0))
         port = so.getsockname()[1]
     procs = []
     for r in range(2):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), CLV_ROOT=ROOT, CLV_D=str(D))
+                   MASTER_PORT=str(port), CLV_ROOT=ROOT, CLV_D=str(D), CLV_PERSISTENT=persistent)
         procs.append(subprocess.Popen([sys.executable, "-c", WORKER], env=env, cwd=ROOT, stdout=subprocess.PIPE,
                                       stderr=subprocess.PIPE, text=True))
     outs = []
@@ -180,16 +262,19 @@ def test_p2p_two_processes_ipc(D):
         assert res["ok"], res
 
 
-def test_p2p_abort_leaves_state_unchanged_and_rollback(monkeypatch):
-    """a persistent launch whose wait times out (here: the peer rank never launches)
-    fails and leaves its rank's state, sweep count and summary sums exactly as before the call;
-    after reconnecting, and after a completed step is undone with clv_rollback on every rank and
-    redone, the run is still bitwise the unsharded one."""
+@pytest.mark.parametrize("persistent", ["1", "0"])
+def test_p2p_abort_leaves_state_unchanged_and_rollback(monkeypatch, persistent):
+    """a call whose wait times out (here: the peer rank never launches) fails and
+    leaves its rank's state, sweep count and summary sums exactly as before the call; after
+    reconnecting, and after a completed step is undone with clv_rollback on every rank and redone,
+    the run is still bitwise the unsharded one.  persistent = "0": the fused exchange (one sweep
+    launch per sweep; the call's launches after the timed-out one return at once)."""
     import torch
     from mcmc_clv_model_amd import _lib
     from mcmc_clv_model_amd import distributed as Dm
     from mcmc_clv_model_amd.sampler import HipSampler, build_problem, make_prior
     monkeypatch.setenv("CLV_WAIT_TIMEOUT_MS", "300")
+    monkeypatch.setenv("CLV_PERSISTENT", persistent)
     p = build_problem(cdnow("full", 23570), ["first_sales_scaled"], 2)
     kw = dict(mcmc=9, burnin=1, thin=1, chains=2, seed=77, draw_sink="summary")
     world = 2
@@ -227,6 +312,7 @@ def test_p2p_abort_leaves_state_unchanged_and_rollback(monkeypatch):
             sh.synchronize()
 
     try:
+        assert all(sh.p2p_info()["persistent"] == (persistent == "1") for sh in shards)
         nd = shards[0].partials()[1]
         gathered = torch.zeros(nd * world, dtype=torch.float64, device="cuda")
         for r, sh in enumerate(shards):
