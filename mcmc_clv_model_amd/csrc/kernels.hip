@@ -1332,12 +1332,10 @@ __device__ __forceinline__ void cust_store(const Cust<D, K>& u, const CustOut<D>
 
 static_assert(BLOCK == EXP_TAB_N, "the sweep kernel stages the exp table with one entry per lane");
 
-// FX: the fused peer exchange (world size > 1 after clv_p2p_connect) compiled in — every Philox
-// instance; it runs only when the launch is sharded.
-#ifndef CLV_FX
-#define CLV_FX 1  // 0: A/B builds without the fused peer exchange
-#endif
-template <int D, int K, bool REPLAY, bool FX = !REPLAY && CLV_FX>
+// FX: the fused peer exchange (world size > 1 after clv_p2p_connect) compiled in — instances of
+// their own, launched for sharded runs only (compiled into the world-size-1 kernels it cost c4 /
+// c5 1.8% / 1.6% per sweep).
+template <int D, int K, bool REPLAY, bool FX>
 __device__ __forceinline__ void sweep_body(const SweepArgs& a) {
   constexpr int NT = BLOCK;
   constexpr int NXY = K * D;
@@ -1622,13 +1620,30 @@ __device__ __forceinline__ void sweep_body(const SweepArgs& a) {
 
 // The sweep kernel at two occupancy targets (an attribute cannot depend on template arguments
 // here): see SweepOcc.
-template <int D, int K, bool REPLAY>
+template <int D, int K, bool REPLAY, bool FX>
 __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
-  sweep_body<D, K, REPLAY>(a);
+  sweep_body<D, K, REPLAY, FX>(a);
 }
-template <int D, int K, bool REPLAY>
+template <int D, int K, bool REPLAY, bool FX>
 __global__ __launch_bounds__(BLOCK, 4) void sweep_kernel_occ4(SweepArgs a) {
-  sweep_body<D, K, REPLAY>(a);
+  sweep_body<D, K, REPLAY, FX>(a);
+}
+
+// One instance per (D, K, REPLAY, FX): the occupancy variant SweepOcc picks (only that one compiled).
+template <int D, int K, bool REPLAY, bool FX>
+hipError_t launch_sweep_t(const SweepArgs& a, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
+  const dim3 grid(a.g.nb_local, a.g.n_chains);
+  const dim3 block(BLOCK);
+  // e0/e1: hipExtLaunchKernelGGL records the dispatch's own start/end timestamps into the events
+  // (no extra marker packets in the stream, unlike hipEventRecord around the launch).
+  if constexpr (SweepOcc<D, K>::value >= 4) {
+    if (e0) hipExtLaunchKernelGGL((sweep_kernel_occ4<D, K, REPLAY, FX>), grid, block, 0, st, e0, e1, 0, a);
+    else hipLaunchKernelGGL((sweep_kernel_occ4<D, K, REPLAY, FX>), grid, block, 0, st, a);
+  } else {
+    if (e0) hipExtLaunchKernelGGL((sweep_kernel<D, K, REPLAY, FX>), grid, block, 0, st, e0, e1, 0, a);
+    else hipLaunchKernelGGL((sweep_kernel<D, K, REPLAY, FX>), grid, block, 0, st, a);
+  }
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2209,20 +2224,13 @@ __global__ void debug_mh_kernel(const int32_t* x, const uint8_t* z, const double
 #endif
 
 hipError_t launch_sweep(const SweepArgs& a, bool replay, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
-  const dim3 grid(a.g.nb_local, a.g.n_chains);
-  const dim3 block(BLOCK);
-  // e0/e1: hipExtLaunchKernelGGL records the dispatch's own start/end timestamps into the events
-  // (no extra marker packets in the stream, unlike hipEventRecord around the launch).
-#define CLV_CASE(DD, KK, RR)                                                                      \
-  if (a.g.D == DD && a.g.K == KK && replay == RR) {                                               \
-    if (SweepOcc<DD, KK>::value >= 4) {                                                           \
-      if (e0) hipExtLaunchKernelGGL((sweep_kernel_occ4<DD, KK, RR>), grid, block, 0, st, e0, e1, 0, a); \
-      else hipLaunchKernelGGL((sweep_kernel_occ4<DD, KK, RR>), grid, block, 0, st, a);            \
-    } else {                                                                                      \
-      if (e0) hipExtLaunchKernelGGL((sweep_kernel<DD, KK, RR>), grid, block, 0, st, e0, e1, 0, a); \
-      else hipLaunchKernelGGL((sweep_kernel<DD, KK, RR>), grid, block, 0, st, a);                 \
-    }                                                                                             \
-    return hipGetLastError();                                                                     \
+  const bool fx = a.fuse && a.g.world_size > 1;  // sharded, fused peer exchange (never in replay mode)
+#define CLV_CASE(DD, KK, RR)                                                      \
+  if (a.g.D == DD && a.g.K == KK && replay == RR) {                               \
+    if constexpr (!RR) {                                                          \
+      if (fx) return launch_sweep_t<DD, KK, RR, true>(a, st, e0, e1);             \
+    }                                                                             \
+    return launch_sweep_t<DD, KK, RR, false>(a, st, e0, e1);                      \
   }
   CLV_FOR_K(CLV_CASE, 2, false)
   CLV_FOR_K(CLV_CASE, 3, false)

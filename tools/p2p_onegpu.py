@@ -1,8 +1,10 @@
 #!/usr/bin/env python
 """Peer-exchange overhead on ONE GPU: W processes (gloo group for the handle exchange) each run a
-1/W shard of the c2 problem through ShardedSampler(exchange="p2p") on the same card, so the
-exchange is IPC-mapped device memory instead of xGMI; compared with the world-size-1 persistent
-run of the same problem (same total workgroups on the card).  Prints one JSON line per rank 0."""
+1/W shard of a bench workload (CLV_P2P_WORKLOAD, default c2) through ShardedSampler(exchange="p2p")
+on the same card, so the exchange is IPC-mapped device memory instead of xGMI; compared with the
+world-size-1 run of the same problem (same total work on the card).  c2: the persistent kernel's
+exchange; c4 (1M customers, shards too large for a resident grid): the sweep kernel's fused
+exchange.  Prints one JSON line per rank 0."""
 import json
 import os
 import socket
@@ -12,6 +14,8 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+WORKLOAD = os.environ.get("CLV_P2P_WORKLOAD", "c2")
+WARM = 200 if WORKLOAD in ("c1", "c2", "c3") else 20
 
 
 def worker(sweeps):
@@ -20,12 +24,12 @@ def worker(sweeps):
     from mcmc_clv_model_amd.sampler import build_problem
     from mcmc_clv_model_amd.distributed import ShardedSampler
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
-    df, D, covs, ch, burnin, mcmc, thin, sink = bench.load_workload("c2")
+    df, D, covs, ch, burnin, mcmc, thin, sink = bench.load_workload(WORKLOAD)
     p = build_problem(df, covs, D)
     dist.init_process_group("gloo")
     ss = ShardedSampler(p, rank=rank, world=world, chains=ch, mcmc=mcmc, burnin=burnin, thin=thin, seed=42,
                         draw_sink=sink, device=0, exchange="p2p", verify_sweeps=8)
-    ss.step(200)
+    ss.step(WARM)
     ss.synchronize()
     dist.barrier()
     t0 = time.perf_counter()
@@ -34,7 +38,8 @@ def worker(sweeps):
     dist.barrier()
     dt = time.perf_counter() - t0
     if rank == 0:
-        print(json.dumps(dict(world=world, us_per_sweep=dt / sweeps * 1e6, exchange=ss.exchange, note=ss.p2p_note)))
+        print(json.dumps(dict(workload=WORKLOAD, world=world, us_per_sweep=dt / sweeps * 1e6, exchange=ss.exchange,
+                              persistent=ss.launch_info()["persistent"], note=ss.p2p_note)))
     if os.environ.get("CLV_LIB_PATH", "").endswith("_stamps.so"):  # level-2 workgroup timeline, one sweep
         import ctypes
         import numpy as np
@@ -66,15 +71,15 @@ def main(world=2, sweeps=3000):
                                        MASTER_PORT=str(port))) for r in range(world)]
     rc = [p.wait(timeout=300) for p in procs]
     assert rc == [0] * world, rc
-    df, D, covs, ch, burnin, mcmc, thin, sink = bench.load_workload("c2")
+    df, D, covs, ch, burnin, mcmc, thin, sink = bench.load_workload(WORKLOAD)
     with HipSampler(build_problem(df, covs, D), mcmc=mcmc, burnin=burnin, thin=thin, chains=ch, seed=42,
                     draw_sink=sink) as s:
-        s.run(200)
+        s.run(WARM)
         s.synchronize()
         t0 = time.perf_counter()
         s.run(sweeps)
         s.synchronize()
-        print(json.dumps(dict(world=1, us_per_sweep=(time.perf_counter() - t0) / sweeps * 1e6)))
+        print(json.dumps(dict(workload=WORKLOAD, world=1, us_per_sweep=(time.perf_counter() - t0) / sweeps * 1e6)))
 
 
 if __name__ == "__main__":
