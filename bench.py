@@ -61,7 +61,12 @@ def algorithmic_bytes(D: int, K: int, stored_frac: float, draw_sink: str) -> flo
     return rd + wr + per_store * stored_frac
 
 
-def committed_traffic(workload: str, sharded: bool, kname: str = "sweep_kernel"):
+def _kernel_matches(name: str, kname: str, D: int, K: int) -> bool:
+    """A profiled kernel is the workload's instance: its name and template arguments <D, K, ...>."""
+    return kname in name and f"<{D}, {K}," in name
+
+
+def committed_traffic(workload: str, sharded: bool, kname: str = "sweep_kernel", D: int = 0, K: int = 0):
     """HBM bytes per sweep-kernel launch from the committed rocprofv3 PMC summary of this workload
     (profiles/*_summary.json written by tools/summarize_profile.py): FETCH_SIZE and WRITE_SIZE
     corrected by the calibration kernels of tools/calib_fetch.hip; None if absent."""
@@ -75,7 +80,7 @@ def committed_traffic(workload: str, sharded: bool, kname: str = "sweep_kernel")
         except Exception:
             continue
         for name, k in d.get("kernels", {}).items():
-            if kname in name and "traffic_bytes" in k:
+            if _kernel_matches(name, kname, D, K) and "traffic_bytes" in k:
                 best = dict(bytes_per_sweep=k["traffic_bytes"] / k.get("sweeps_per_dispatch", 1),
                             source=os.path.basename(path),
                             counters="FETCH_SIZE x %.2f + WRITE_SIZE x %.2f (calibrated, tools/calib_fetch.hip)"
@@ -87,7 +92,7 @@ N_SIMDS = 1024  # 256 CUs x 4 SIMDs (MI355X_MICROARCH.md)
 N_XCDS = 8      # GRBM_GUI_ACTIVE is summed over the 8 XCDs
 
 
-def committed_counters(workload: str, sharded: bool, kname: str = "sweep_kernel"):
+def committed_counters(workload: str, sharded: bool, kname: str = "sweep_kernel", D: int = 0, K: int = 0):
     """Counter evidence for the roofline's `bound` from the committed rocprofv3 summary of this
     workload (tools/summarize_profile.py): VALU busy = SQ_ACTIVE_INST_VALU (quad-cycles, x4) summed
     over the kernel's waves / (1,024 SIMDs x the dispatch's cycles, GRBM_GUI_ACTIVE / 8 XCDs) — the
@@ -102,7 +107,7 @@ def committed_counters(workload: str, sharded: bool, kname: str = "sweep_kernel"
         except Exception:
             continue
         for name, k in d.get("kernels", {}).items():
-            if kname in name and "valu_active_quadcycles_per_wave" in k and k.get("grbm_gui_active"):
+            if _kernel_matches(name, kname, D, K) and "valu_active_quadcycles_per_wave" in k and k.get("grbm_gui_active"):
                 cycles = k["grbm_gui_active"] / N_XCDS
                 busy = 4.0 * k["valu_active_quadcycles_per_wave"] * k["waves"] / (N_SIMDS * cycles)
                 best = dict(valu_busy_frac=round(busy, 4),
@@ -404,14 +409,14 @@ def main():
                             timed_launches=kt["sweep_launches"] // spl,
                             events=("the timed region's launch" if live else
                                     f"a roofline pass of {n_t} further sweeps, one event pair per launch"))
-            tr = committed_traffic(a.workload, sharded and not p2p, kname)
+            tr = committed_traffic(a.workload, sharded and not p2p, kname, D, K)
             if tr:  # HBM bytes per launch (calibrated PMC), per sweep x sweeps per launch
                 roofline["traffic"] = round(tr["bytes_per_sweep"] * spl)
                 roofline["traffic_source"] = f"{tr['source']}: {tr['counters']}"
             if kt["hyper_launches"]:
                 roofline["hyper_kernel_us"] = round(kt["hyper_ms"] / kt["hyper_launches"] * 1e3, 3)
             # bound: from the counters (HBM traffic rate vs peak, VALU busy share), not assumed
-            ev = committed_counters(a.workload, sharded and not p2p, kname) or {}
+            ev = committed_counters(a.workload, sharded and not p2p, kname, D, K) or {}
             if roofline["traffic"] is not None:
                 ev["hbm_traffic_frac"] = round(roofline["traffic"] / t_launch / 1e9 / HBM_PEAK_GBS, 4)
             if ev.get("hbm_traffic_frac", 0.0) >= 0.6:

@@ -33,16 +33,31 @@
 #ifndef SWEEP_REDUCE_CHUNK
 #define SWEEP_REDUCE_CHUNK 8  // statistics formed and reduced per chunk in the customer workgroups
 #endif
-// sweep_kernel __launch_bounds__ minimum workgroups per CU: 4 (<= 128 VGPRs, 4 waves per SIMD) for
-// the bivariate instances up to K = 5 — c4 (1M, K=5) 104.4 -> 101.0 us per sweep — and the
-// compiler's choice (168 VGPRs, 3 waves) for the trivariate ones, where the 128-register cap
-// spills (c5 151 -> 160 us).  SWEEP_MIN_BLOCKS overrides (A/B builds).
+// sweep_kernel __launch_bounds__ minimum workgroups per CU: 4 (<= 128 VGPRs, 4 waves per SIMD)
+// for the bivariate instances (but K = 6, whose 128-register cap spills): c4 104.4 -> 101.0 us
+// per sweep (round 1), and 101.5 -> 100.3 against the compiler's choice now.  The trivariate
+// ones keep the compiler's choice: with the covariates in LDS (CovLds, K >= 6) c5 needs 127 VGPRs
+// and runs 4 waves per SIMD either way, but the cap's scheduling cost it 146.2 -> 160.5 us
+// (measured).  SWEEP_MIN_BLOCKS overrides (A/B builds).
+template <int D, int K>
+struct SweepOcc;
+
+// Launch-per-sweep instances whose covariate rows live in LDS (Cust CL) — K >= 6, where the
+// covariates' registers decided the occupancy.  SWEEP_COV_LDS_MIN_K overrides (A/B builds).
+#ifndef SWEEP_COV_LDS_MIN_K
+#define SWEEP_COV_LDS_MIN_K 6
+#endif
+template <int D, int K>
+struct CovLds {
+  static constexpr bool value = K >= SWEEP_COV_LDS_MIN_K;
+};
+
 template <int D, int K>
 struct SweepOcc {  // waves per SIMD the launched instance is compiled for (sweep_kernel_occ4 if 4)
 #ifdef SWEEP_MIN_BLOCKS
   static constexpr int value = SWEEP_MIN_BLOCKS;  // 4: every instance occ4, else none
 #else
-  static constexpr int value = (D == 2 && K <= 5) ? 4 : 1;
+  static constexpr int value = (D == 2 && K != 6) ? 4 : 1;
 #endif
 };
 
@@ -957,11 +972,19 @@ __device__ __forceinline__ bool wait_expired(const SweepArgs& a, uint64_t t0, ui
 // Sweep kernel
 // ---------------------------------------------------------------------------------------------
 // One customer's sweep state (per lane and task).
-template <int D, int K>
+// CL (covariates in LDS): the launch-per-sweep kernel keeps a lane's covariate row in its
+// workgroup's LDS ([k-1][BLOCK], each lane reads back only what it wrote — no barrier) instead of
+// K-1 register pairs live across the whole MH phase (c5, K = 9: 16 VGPRs).
+template <int D, int K, bool CL = false>
 struct Cust {
   int64_t i;          // local customer index (clamped to a valid row for inactive tasks)
   bool active;
-  double xr[K];       // [1, covariates]
+  double xr_[CL ? 1 : K];  // [1, covariates] in registers (CL: unused)
+  double* cl;         // CL: this lane's covariate column in LDS (element k-1 at cl[(k-1) * BLOCK])
+  __device__ __forceinline__ double x(int k) const {
+    if constexpr (CL) return k == 0 ? 1.0 : cl[(k - 1) * BLOCK];
+    else return xr_[k];
+  }
   double tx, T, xm;
   int32_t xi;         // x as loaded (converted in cust_prepare, so the load is not waited for early)
   double lam, mu, eta, tau;
@@ -974,15 +997,20 @@ struct Cust {
 
 // Phase A1: the customer's loads (CBS row, covariates, state), issued before the workgroup's
 // exp-table barrier so their latency overlaps it.
-template <int D, int K>
-__device__ __forceinline__ void cust_load(Cust<D, K>& u, const SweepArgs& a, int c) {
+template <int D, int K, bool CL>
+__device__ __forceinline__ void cust_load(Cust<D, K, CL>& u, const SweepArgs& a, int c) {
   const Geometry& g = a.g;
   const int64_t i = u.i;
   u.tx = a.tx[i];
   u.T = a.T[i];
-  u.xr[0] = 1.0;
+  if constexpr (CL) {
 #pragma unroll
-  for (int k = 1; k < K; ++k) u.xr[k] = a.cov[(int64_t)(k - 1) * g.n + i];
+    for (int k = 1; k < K; ++k) u.cl[(k - 1) * BLOCK] = a.cov[(int64_t)(k - 1) * g.n + i];
+  } else {
+    u.xr_[0] = 1.0;
+#pragma unroll
+    for (int k = 1; k < K; ++k) u.xr_[k] = a.cov[(int64_t)(k - 1) * g.n + i];
+  }
   const int64_t ci = (int64_t)c * g.n + i;
   u.lam = a.lam[ci];
   u.mu = a.mu[ci];
@@ -993,8 +1021,8 @@ __device__ __forceinline__ void cust_load(Cust<D, K>& u, const SweepArgs& a, int
 // Phase A2a (bi:193-227): draw_z, draw_tau and the log-scale state — independent of the level-2
 // state (beta, Sigma), so the persistent kernel runs it for sweep s+1 while sweep s's level-2
 // draw is still in flight.
-template <int D, int K, bool REPLAY>
-__device__ __forceinline__ void cust_ztau(Cust<D, K>& u, const SweepArgs& a, int64_t s, uint32_t k0, uint32_t k1,
+template <int D, int K, bool REPLAY, bool CL>
+__device__ __forceinline__ void cust_ztau(Cust<D, K, CL>& u, const SweepArgs& a, int64_t s, uint32_t k0, uint32_t k1,
                                           const double* tape, const double* exp_tab) {
   const Geometry& g = a.g;
   const int64_t i = u.i;
@@ -1059,14 +1087,14 @@ __device__ __forceinline__ void cust_ztau(Cust<D, K>& u, const SweepArgs& a, int
 
 // Phase A2b (bi:280-290): log-posterior constants from (beta, Sigma) and the current point's
 // log posterior.
-template <int D, int K, bool REPLAY>
-__device__ __forceinline__ void cust_coeffs(Cust<D, K>& u, const double* H, const double* exp_tab) {
+template <int D, int K, bool REPLAY, bool CL>
+__device__ __forceinline__ void cust_coeffs(Cust<D, K, CL>& u, const double* H, const double* exp_tab) {
   // ---- _draw_level_1 (bi:268-339): mv_mean = X @ beta (bi:284)
   double m0 = 0.0, m1 = 0.0;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    m0 += u.xr[k] * H[H_BETA + k * D + 0];
-    m1 += u.xr[k] * H[H_BETA + k * D + 1];
+    m0 += u.x(k) * H[H_BETA + k * D + 0];
+    m1 += u.x(k) * H[H_BETA + k * D + 1];
   }
   LPConst& lc = u.lc;
   lc.m0 = m0;
@@ -1089,8 +1117,8 @@ __device__ __forceinline__ void cust_coeffs(Cust<D, K>& u, const double* H, cons
 }
 
 // Phase A2 (bi:193-227, bi:280-290): both of the above.
-template <int D, int K, bool REPLAY>
-__device__ __forceinline__ void cust_prepare(Cust<D, K>& u, const SweepArgs& a, int c, int64_t s, const double* H,
+template <int D, int K, bool REPLAY, bool CL>
+__device__ __forceinline__ void cust_prepare(Cust<D, K, CL>& u, const SweepArgs& a, int c, int64_t s, const double* H,
                                              uint32_t k0, uint32_t k1, const double* tape, const double* exp_tab) {
   (void)c;
   cust_ztau<D, K, REPLAY>(u, a, s, k0, k1, tape, exp_tab);
@@ -1113,8 +1141,8 @@ __device__ __forceinline__ double clip70_fma(double a, double b, double c) {
 // pm <= 5 and exp(plp - cur) > u  <=>  plp > cur + log(u)  (cur = -inf accepts any finite one;
 // cur + log u is formed off the dependent chain, alongside the proposal; a padded step's
 // log u = +inf gives +inf or NaN there, never accepted).
-template <int D, int K>
-__device__ __forceinline__ void mh_step(Cust<D, K>& u, double s00, double s11, float t_l, float t_m, float l_u,
+template <int D, int K, bool CL>
+__device__ __forceinline__ void mh_step(Cust<D, K, CL>& u, double s00, double s11, float t_l, float t_m, float l_u,
                                         const double* exp_tab) {
   const double thr = u.cur + (double)l_u;
   const double pl = clip70_fma(s00, (double)t_l, u.ll);
@@ -1132,8 +1160,8 @@ __device__ __forceinline__ void mh_step(Cust<D, K>& u, double s00, double s11, f
 // the next chunk's variates form one branch-free basic block, so the scheduler can interleave
 // that work with the dependent fp64 accept/reject chain.  The last chunk's steps beyond S are
 // padded with log U = +inf (never accepted: the state is unchanged) instead of a branch.
-template <int D, int K>
-__device__ __forceinline__ void mh_run(Cust<D, K>& cu, const SlotPhilox& ph, double s00, double s11, int S,
+template <int D, int K, bool CL>
+__device__ __forceinline__ void mh_run(Cust<D, K, CL>& cu, const SlotPhilox& ph, double s00, double s11, int S,
                                        const double* exp_tab) {
   constexpr int MC = MH_CHUNK_STEPS;
   const int n_chunks = (S + MC - 1) / MC;
@@ -1197,8 +1225,8 @@ __device__ __forceinline__ void mh_pre_variates(const SlotPhilox& ph, int S, con
   }
 }
 
-template <int D, int K>
-__device__ __forceinline__ void mh_run_pre(Cust<D, K>& cu, const PreVariates& v, double s00, double s11, int S,
+template <int D, int K, bool CL>
+__device__ __forceinline__ void mh_run_pre(Cust<D, K, CL>& cu, const PreVariates& v, double s00, double s11, int S,
                                            const double* exp_tab) {
   constexpr int MC = MH_CHUNK_STEPS;
 #pragma unroll
@@ -1224,8 +1252,8 @@ struct CustOut {
   double lam, mu, eta, lgl, lgm;
 };
 
-template <int D, int K, bool REPLAY>
-__device__ __forceinline__ CustOut<D> cust_finish(Cust<D, K>& u, const SweepArgs& a, int64_t s, bool stored,
+template <int D, int K, bool REPLAY, bool CL>
+__device__ __forceinline__ CustOut<D> cust_finish(Cust<D, K, CL>& u, const SweepArgs& a, int64_t s, bool stored,
                                                   const double* H, uint32_t k0, uint32_t k1, const double* tape,
                                                   const double* exp_tab, StatGen<D, K>& st) {
   const Geometry& g = a.g;
@@ -1243,7 +1271,7 @@ __device__ __forceinline__ CustOut<D> cust_finish(Cust<D, K>& u, const SweepArgs
   if constexpr (D == 3) {
     double m2 = 0.0;
 #pragma unroll
-    for (int k = 0; k < K; ++k) m2 += u.xr[k] * H[H_BETA + k * D + 2];
+    for (int k = 0; k < K; ++k) m2 += u.x(k) * H[H_BETA + k * D + 2];
     const double post_var = H[H_POSTVAR];
     const double post_mean = post_var * (a.log_s[i] / H[H_OMEGA2] + m2 / H[H_S22]);
     double zeta;
@@ -1279,7 +1307,7 @@ __device__ __forceinline__ CustOut<D> cust_finish(Cust<D, K>& u, const SweepArgs
   // ---- sufficient statistics X'Y (K x D), Y'Y (upper triangle), likelihood term: formed in the
   // workgroup reduction (block_reduce_gen), a few at a time
 #pragma unroll
-  for (int k = 0; k < K; ++k) st.xr[k] = u.xr[k];
+  for (int k = 0; k < K; ++k) st.xr[k] = u.x(k);
 #pragma unroll
   for (int d = 0; d < D; ++d) st.Y[d] = Y[d];
   st.lik = lik;
@@ -1289,8 +1317,8 @@ __device__ __forceinline__ CustOut<D> cust_finish(Cust<D, K>& u, const SweepArgs
 
 // Phase C2: storage (bi:402-412, tri:539-571) — issued after the workgroup's partial has been
 // handed off, so the hand-off's store drain does not wait for them — and the carried state.
-template <int D, int K>
-__device__ __forceinline__ void cust_store(const Cust<D, K>& u, const CustOut<D>& o, const SweepArgs& a, int c,
+template <int D, int K, bool CL>
+__device__ __forceinline__ void cust_store(const Cust<D, K, CL>& u, const CustOut<D>& o, const SweepArgs& a, int c,
                                            int64_t s, bool stored, bool store_state) {
   const Geometry& g = a.g;
   const int64_t i = u.i;
@@ -1360,7 +1388,10 @@ __device__ __forceinline__ void sweep_body(const SweepArgs& a) {
   }
   // The customer's loads go out first, so that their latency, the exp table's and the sweep
   // index's overlap (one memory round trip before compute instead of several).
-  Cust<D, K> cu;
+  constexpr bool CL = CovLds<D, K>::value;
+  __shared__ double cov_s[CL ? (K - 1) * BLOCK : 1];
+  Cust<D, K, CL> cu;
+  cu.cl = cov_s + threadIdx.x;
   {
     const int64_t i = (int64_t)b * BLOCK + threadIdx.x;
     cu.active = i < g.n;
@@ -1446,7 +1477,7 @@ __device__ __forceinline__ void sweep_body(const SweepArgs& a) {
     const double s11 = H[H_S11];
     if constexpr (REPLAY) {
       {
-        Cust<D, K>& u = cu;
+        auto& u = cu;
         for (int j = 0; j < g.S; ++j) {
           const double tl = tape[(int64_t)(2 + 3 * j) * g.n + u.i];
           const double tm = tape[(int64_t)(3 + 3 * j) * g.n + u.i];
@@ -1572,38 +1603,44 @@ __device__ __forceinline__ void sweep_body(const SweepArgs& a) {
         double* p1 = (double*)mb + (u1 / g.units_per_rank) * mail_rank + (u1 % g.units_per_rank) * NS;
         const double* q0 = h0 ? p0 : mb;
         const double* q1 = h1 ? p1 : mb;
-        double v0[NS], v1[NS];
         __shared__ uint32_t s_fx_abort;
         if (threadIdx.x == 0) s_fx_abort = 0;
         __syncthreads();
-        {
+        // statistics in chunks of FXC (all NS at once for small NS): the polled values of a chunk
+        // and the lane's finished sums are live together, not 2 NS polled values (c5: NS = 34)
+        constexpr int FXC = NS <= 16 ? NS : 12;
+        double acc[NS];
+        bool timed_out = false;
+#pragma unroll
+        for (int j0 = 0; j0 < NS; j0 += FXC) {
+          double v0[FXC], v1[FXC];
           const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-          for (uint32_t poll = 0;; ++poll) {
+          for (uint32_t poll = 0; !timed_out; ++poll) {
             bool ok = true;
 #pragma unroll
-            for (int j = 0; j < NS; ++j) {
-              v0[j] = ld_sys(q0 + j);
-              v1[j] = ld_sys(q1 + j);
+            for (int q = 0; q < FXC; ++q) {
+              if (j0 + q < NS) {
+                v0[q] = ld_sys(q0 + j0 + q);
+                v1[q] = ld_sys(q1 + j0 + q);
+                ok = ok & (!h0 | slot_full(v0[q])) & (!h1 | slot_full(v1[q]));
+              }
             }
-#pragma unroll
-            for (int j = 0; j < NS; ++j) ok = ok & (!h0 | slot_full(v0[j])) & (!h1 | slot_full(v1[j]));
             if (__all(ok)) break;
-            if (wait_expired(a, t0, poll)) {
-              s_fx_abort = 1;
-              break;
+            if (wait_expired(a, t0, poll)) timed_out = true;
+            else __builtin_amdgcn_s_sleep(1);
+          }
+#pragma unroll
+          for (int q = 0; q < FXC; ++q) {
+            if (j0 + q < NS) {
+              acc[j0 + q] = 0.0;
+              if (h0) acc[j0 + q] += v0[q];
+              if (h1) acc[j0 + q] += v1[q];
             }
-            __builtin_amdgcn_s_sleep(1);
           }
         }
+        if (timed_out) s_fx_abort = 1;
         __syncthreads();
         if (!s_fx_abort) {
-          double acc[NS];
-#pragma unroll
-          for (int j = 0; j < NS; ++j) {
-            acc[j] = 0.0;
-            if (h0) acc[j] += v0[j];
-            if (h1) acc[j] += v1[j];
-          }
 #pragma unroll
           for (int j = 0; j < NS; ++j) {
             if (h0) st_sys(p0 + j, slot_empty());
@@ -2189,7 +2226,7 @@ __global__ void debug_mh_kernel(const int32_t* x, const uint8_t* z, const double
   H[H_P01] = prec[1];
   H[H_P11] = prec[2];
   Cust<2, 1> u;
-  u.xr[0] = 1.0;
+  u.xr_[0] = 1.0;
   u.xm = (double)x[i];
   u.z = z[i] != 0;
   u.lc.xm = u.xm;
