@@ -284,6 +284,9 @@ def main():
                     help="BASELINE multi-GPU configurations also measured at this N (c4 strong, c5 weak "
                          "scaling), reported under `configs`; '' to skip")
     ap.add_argument("--scaling-steps", type=int, default=200)
+    ap.add_argument("--one-gpu-rehearsal", action="store_true",
+                    help="world size > 1 on a one-GPU box: every rank on device 0, gloo process group (the "
+                         "exchange paths are exercised; the numbers are not a scaling measurement)")
     ap.add_argument("--cpu-baseline-child", action="store_true")
     ap.add_argument("--cpu-warm", type=int, default=20)
     ap.add_argument("--cpu-timed", type=int, default=200)
@@ -298,6 +301,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.one_gpu_rehearsal:
+        local_rank = 0
+        a.graph_chunk = 0  # (a gloo exchange cannot be captured in a graph)
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
     dist = None
@@ -309,7 +315,10 @@ def main():
         os.environ.setdefault("MASTER_PORT", "29533")
         os.environ.setdefault("RANK", str(rank))
         os.environ.setdefault("WORLD_SIZE", str(world))
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
+        if a.one_gpu_rehearsal:  # RCCL refuses two ranks on one GPU
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
 
     from mcmc_clv_model_amd import _lib
     from mcmc_clv_model_amd.sampler import HipSampler, build_problem
