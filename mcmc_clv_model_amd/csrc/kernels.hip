@@ -27,6 +27,9 @@
 #ifndef CLV_L2_OPAQUE
 #define CLV_L2_OPAQUE(P) (P)          // level-2 lane bookkeeping recomputed per sweep (not hoisted)
 #endif
+#ifndef CLV_L2_LANE0_MAX
+#define CLV_L2_LANE0_MAX 6  // persistent kernel (world size 1): one-lane level-2 algebra up to K*D (c3, K*D = 9: the element-parallel form 15.31 -> 15.11 us)
+#endif
 #ifndef PERSIST_REDUCE_GEN
 #define PERSIST_REDUCE_GEN 1  // persistent kernel: statistics formed chunk-wise in the reduction
 #endif
@@ -1249,13 +1252,22 @@ __device__ __forceinline__ void mh_run_pre(Cust<D, K, CL>& cu, const PreVariates
 // sweeps (bi:423-427) and the customer's sufficient statistics into acc.
 template <int D>
 struct CustOut {
-  double lam, mu, eta, lgl, lgm;
+  double lam, mu, eta, lgl, lgm, leta;  // leta = log(eta) (Philox mode: the exponent itself)
 };
+
+// draw_eta's standard normal (tri:333 rng.normal), Philox mode: fp64 Box-Muller from the
+// customer's SLOT_ETA block.  Independent of the state, so the persistent kernel draws it for
+// sweep s+1 in the level-2 hand-off window (with the MH variates), off the sweep's serial path.
+__device__ __forceinline__ double eta_normal(uint32_t k0, uint32_t k1, uint32_t gi, int64_t s) {
+  const u32x4 r = customer_block(k0, k1, gi, (uint32_t)s, SLOT_ETA);
+  return sqrt(-2.0 * log(u53_open0(r.x, r.y))) * cospi(2.0 * u53(r.z, r.w));
+}
 
 template <int D, int K, bool REPLAY, bool CL>
 __device__ __forceinline__ CustOut<D> cust_finish(Cust<D, K, CL>& u, const SweepArgs& a, int64_t s, bool stored,
                                                   const double* H, uint32_t k0, uint32_t k1, const double* tape,
-                                                  const double* exp_tab, StatGen<D, K>& st) {
+                                                  const double* exp_tab, StatGen<D, K>& st,
+                                                  const double* zeta_pre = nullptr) {
   const Geometry& g = a.g;
   const int64_t i = u.i;
   // bi:337-338 (state back to natural scale).  Replay reproduces the reference's exp/log round
@@ -1267,7 +1279,7 @@ __device__ __forceinline__ CustOut<D> cust_finish(Cust<D, K, CL>& u, const Sweep
   } else {
     exp_fast2(u.ll, u.lm, exp_tab, lam, mu);
   }
-  double eta = 1.0, Y[D];
+  double eta = 1.0, leta = 0.0, Y[D];
   if constexpr (D == 3) {
     double m2 = 0.0;
 #pragma unroll
@@ -1278,14 +1290,21 @@ __device__ __forceinline__ CustOut<D> cust_finish(Cust<D, K, CL>& u, const Sweep
     if constexpr (REPLAY) {
       zeta = tape[(int64_t)(2 + 3 * g.S) * g.n + i];
     } else {
-      const u32x4 r = customer_block(k0, k1, u.gi, (uint32_t)s, SLOT_ETA);
-      zeta = sqrt(-2.0 * log(u53_open0(r.x, r.y))) * cospi(2.0 * u53(r.z, r.w));
+      zeta = zeta_pre ? *zeta_pre : eta_normal(k0, k1, u.gi, s);
     }
-    eta = exp(post_mean + H[H_SQRT_POSTVAR] * zeta);
+    const double xe = post_mean + H[H_SQRT_POSTVAR] * zeta;
+    if constexpr (REPLAY) {
+      eta = exp(xe);
+      leta = log(eta);  // tri:534 (level 2 sees log of the natural-scale draw)
+    } else {  // Philox mode: the table exp, and log(exp(x)) = x (within an ulp, as for lambda, mu)
+      if (__builtin_fabs(xe) <= 700.0) eta = exp_fast(xe, exp_tab);
+      else eta = exp(xe);
+      leta = xe;
+    }
     // tri: level 2 sees log(lambda) before the storage round trip (tri:529-536 before :542)
     Y[0] = REPLAY ? log(lam) : u.ll;
     Y[1] = REPLAY ? log(mu) : u.lm;
-    Y[2] = log(eta);
+    Y[2] = leta;
   }
   double lik = 0.0, lgl = 0.0, lgm = 0.0;
   if (stored) {
@@ -1312,7 +1331,7 @@ __device__ __forceinline__ CustOut<D> cust_finish(Cust<D, K, CL>& u, const Sweep
   for (int d = 0; d < D; ++d) st.Y[d] = Y[d];
   st.lik = lik;
   st.on = true;
-  return CustOut<D>{lam, mu, eta, lgl, lgm};
+  return CustOut<D>{lam, mu, eta, lgl, lgm, leta};
 }
 
 // Phase C2: storage (bi:402-412, tri:539-571) — issued after the workgroup's partial has been
@@ -1343,7 +1362,7 @@ __device__ __forceinline__ void cust_store(const Cust<D, K, CL>& u, const CustOu
       sm[CLV_SUM_MU2 * g.n] += o.mu * o.mu;
       if constexpr (D == 3) {
         sm[CLV_SUM_ETA * g.n] += o.eta;
-        sm[CLV_SUM_LOG_ETA * g.n] += log(o.eta);
+        sm[CLV_SUM_LOG_ETA * g.n] += o.leta;
       }
       sm[CLV_SUM_MU_CAPPED * g.n] += fmin(o.mu, CLV_SUMMARY_MU_CAP);  // np.clip(mu, None, 0.05)
       sm[CLV_SUM_TAU * g.n] += u.tau;
@@ -1938,7 +1957,7 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
     // 5. the draw (wavefront 0) while the resets drain
     // P2P: the one-lane form only for the smallest K*D (its registers, added to the exchange's,
     // spilled the peer kernel at K*D = 10); the element-parallel form gives the same bits
-    level2_draw<D, K, P2P ? 6 : 12>(tot, var_iw, var_chi, var_noise, false, &l2, l2.Ai);
+    level2_draw<D, K, P2P ? 6 : CLV_L2_LANE0_MAX>(tot, var_iw, var_chi, var_noise, false, &l2, l2.Ai);
     CLV_P_STAMP(a.stamps, wgi, 7, stp);
     if (tid == 0) {
       double Sig[D][D];
@@ -2000,6 +2019,7 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
   // customer workgroups: the drawn-ahead MH variates; the level-2 workgroup (P2P): its unit partials
   __shared__ __attribute__((aligned(16))) char pool[PRE_LDS_BYTES];
   static_assert(UMAIL * sizeof(double) <= PRE_LDS_BYTES, "the level-2 unit partials share the variates' LDS");
+  __shared__ double zeta_lds[D == 3 ? BLOCK : 1];  // draw_eta's normal of the next sweep (trivariate)
   const Geometry& g = a.g;
   int c = blockIdx.y, b = blockIdx.x;
   if (a.wg_map) {  // placement (capi.hip persist_wg_map): same-chain workgroups share CUs
@@ -2038,6 +2058,9 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
   const bool pre = a.pre_variates && g.S <= PRE_STEPS;
   const PreVariates pv{(float2*)pool, (float*)(pool + PRE_STEPS * BLOCK * 8), tid};
   if (cu.active && pre) mh_pre_variates(SlotPhilox(k0, k1, cu.gi, (uint32_t)s_first), g.S, pv);
+  if constexpr (D == 3) {
+    if (cu.active && pre) zeta_lds[tid] = eta_normal(k0, k1, cu.gi, s_first);
+  }
   const double* hyp_c = a.hyp2 + (int64_t)c * HS;
   for (int64_t it = 0; it < n_sweeps; ++it) {
     // Philox products of the customer counter word are the same every sweep; hoisted out of the
@@ -2079,7 +2102,11 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
       if (pre) mh_run_pre(cu, pv, s00, s11, g.S, exp_tab);
       else mh_run(cu, SlotPhilox(k0, k1, cu.gi, (uint32_t)s), s00, s11, g.S, exp_tab);
       CLV_P_STAMP(a.stamps, wgi, 3, stp);
-      out = cust_finish<D, K, false>(cu, a, s, stored, Hs, k0, k1, nullptr, exp_tab, st);
+      if constexpr (D == 3) {
+        if (!pre) zeta_lds[tid] = eta_normal(k0, k1, cu.gi, s);  // (not drawn ahead: S > PRE_STEPS)
+      }
+      out = cust_finish<D, K, false>(cu, a, s, stored, Hs, k0, k1, nullptr, exp_tab, st,
+                                     D == 3 ? &zeta_lds[tid] : nullptr);
     }
     CLV_P_STAMP(a.stamps, wgi, 4, stp);
 #if PERSIST_REDUCE_GEN
@@ -2104,6 +2131,9 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
       if (it + 1 < n_sweeps) {
         cust_ztau<D, K, false>(cu, a, s + 1, k0, k1, nullptr, exp_tab);
         if (pre) mh_pre_variates(SlotPhilox(k0, k1, cu.gi, (uint32_t)(s + 1)), g.S, pv);
+        if constexpr (D == 3) {
+          if (pre) zeta_lds[tid] = eta_normal(k0, k1, cu.gi, s + 1);
+        }
       }
     }
     CLV_P_STAMP(a.stamps, wgi, 6, stp);
