@@ -442,7 +442,8 @@ def main():
     kern.close()
     extra = {}
     for name in [c for c in a.scaling_configs.split(",") if c]:
-        extra[name] = measure_config(name, world, rank, local_rank, dist, a.scaling_steps, 20, a.graph_chunk,
+        # warm-up of 80 sweeps: the launch-per-sweep path captures its 64-sweep hipGraph on first use
+        extra[name] = measure_config(name, world, rank, local_rank, dist, a.scaling_steps, 80, a.graph_chunk,
                                      a.exchange if world > 1 else "rccl")
 
     if rank == 0:
