@@ -361,7 +361,8 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     run(a.steps)                      # timed region: persistent launch / hipGraph replay / sharded steps
-    sync()
+    if sharded:
+        sync()                        # (HipSampler.run returns when its launches are done)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
