@@ -469,6 +469,25 @@ def fit(p: Problem, *, mcmc: int, burnin: int, thin: int, chains: int, seed, tra
         s.close()
 
 
+def multi_plan(chains: int, n_dev: int, draw_sink: str, shard: str = "auto"):
+    """How :func:`fit_multi` spreads a run over ``n_dev`` devices: ("chains", [(first chain,
+    chains), ...] one group per device used) or ("customers", None).  "auto" takes chain groups
+    when the chains divide evenly over the devices and the sink does not pool chains."""
+    if shard not in ("auto", "chains", "customers"):
+        raise ValueError("shard must be 'auto', 'chains' or 'customers'")
+    if chains < 1 or n_dev < 1:
+        raise ValueError("chains and devices must be >= 1")
+    if shard == "auto":
+        shard = "chains" if (chains % n_dev == 0 and draw_sink != "summary+pct") else "customers"
+    if shard == "chains" and draw_sink == "summary+pct":
+        raise ValueError("draw_sink='summary+pct' pools every chain's draws: use shard='customers'")
+    if shard == "customers":
+        return shard, None
+    n_grp = min(n_dev, chains)
+    sizes = [chains // n_grp + (1 if g < chains % n_grp else 0) for g in range(n_grp)]
+    return shard, [(sum(sizes[:g]), sizes[g]) for g in range(n_grp)]
+
+
 def fit_multi(p: Problem, *, mcmc: int, burnin: int, thin: int, chains: int, seed, trace: int, n_mh_steps: int,
               draw_sink: str, devices: Sequence[int], shard: str = "auto", exchange: str = "auto") -> dict:
     """One run over several devices of this process (SURVEY §8b ``devices=``), same output as the
@@ -485,19 +504,14 @@ def fit_multi(p: Problem, *, mcmc: int, burnin: int, thin: int, chains: int, see
       "summary+pct", whose percentiles pool all chains), else customers."""
     import threading
     n_dev = len(devices)
-    if shard not in ("auto", "chains", "customers"):
-        raise ValueError("shard must be 'auto', 'chains' or 'customers'")
-    if shard == "auto":
-        shard = "chains" if (chains % n_dev == 0 and draw_sink != "summary+pct") else "customers"
-    if shard == "chains" and draw_sink == "summary+pct":
-        raise ValueError("draw_sink='summary+pct' pools every chain's draws: use shard='customers'")
+    shard, groups = multi_plan(chains, n_dev, draw_sink, shard)
     seed = resolve_seed(seed)
     total = burnin + mcmc
     kw = dict(mcmc=mcmc, burnin=burnin, thin=thin, seed=seed, n_mh_steps=n_mh_steps, draw_sink=draw_sink)
     if shard == "chains":
-        n_grp = min(n_dev, chains)
-        sizes = [chains // n_grp + (1 if g < chains % n_grp else 0) for g in range(n_grp)]
-        firsts = [sum(sizes[:g]) for g in range(n_grp)]
+        n_grp = len(groups)
+        firsts = [g[0] for g in groups]
+        sizes = [g[1] for g in groups]
         samplers = []
         try:
             for g in range(n_grp):

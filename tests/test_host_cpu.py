@@ -289,3 +289,22 @@ def test_bench_scaling_workloads(world, monkeypatch):
         pl = D.plan(n, world)
         spans = [pl.shard(r) for r in range(world)]
         assert spans[0][0] == 0 and spans[-1][1] == n
+
+
+def test_multi_device_plan():
+    """devices= (sampler.multi_plan): chain groups cover every chain once, in order, one group per
+    device used; 'auto' shards customers when chains do not divide evenly or the sink pools chains."""
+    from mcmc_clv_model_amd.sampler import multi_plan
+    for chains in range(1, 10):
+        for n_dev in range(1, 9):
+            mode, groups = multi_plan(chains, n_dev, "full", "chains")
+            assert mode == "chains" and len(groups) == min(chains, n_dev)
+            assert [c for f, k in groups for c in range(f, f + k)] == list(range(chains))
+            assert max(k for _, k in groups) - min(k for _, k in groups) <= 1
+            auto = multi_plan(chains, n_dev, "full")[0]
+            assert auto == ("chains" if chains % n_dev == 0 else "customers")
+    assert multi_plan(4, 2, "summary+pct")[0] == "customers"
+    with pytest.raises(ValueError, match="summary\\+pct"):
+        multi_plan(4, 2, "summary+pct", "chains")
+    with pytest.raises(ValueError, match="shard must be"):
+        multi_plan(4, 2, "full", "rows")
