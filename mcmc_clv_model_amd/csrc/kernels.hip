@@ -1135,8 +1135,8 @@ __device__ __forceinline__ void cust_prepare(Cust<D, K, CL>& u, const SweepArgs&
 __device__ __forceinline__ double clip70_fma(double a, double b, double c) {
   double r, lo = -70.0, hi = 70.0;
   asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(r), "v"(lo));
-  asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(r), "v"(hi));
+  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(r), "s"(lo));  // bounds from SGPRs: no per-step
+  asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(r), "s"(hi));  // v_mov_b64 into VGPRs
   return r;
 }
 
