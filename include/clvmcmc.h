@@ -228,6 +228,9 @@ int clv_debug_hyper_variates(uint64_t seed, int32_t chain, uint32_t sweep, doubl
                              double* chi2, double* normals);
 /* The Philox-mode MH step's fp64 exp (csrc/fastmath.h, |x| <= 700) on n values. */
 int clv_debug_exp(const double* x, int64_t n, double* out);
+/* The Philox-mode fp64 log (csrc/fastmath.h log_fast, x > 0 normal) on n values: the z/tau
+ * draw's logs (bi:200-225) and the eta normal's radius. */
+int clv_debug_log(const double* x, int64_t n, double* out);
 /* One Philox-mode MH step exactly as the sweep kernels run it (bi:291-335: log posterior with the
  * Q3 cap, fma + clip proposal, accept iff pm <= 5 and plp > cur + log U), on n independent lanes.
  * Per lane: x, z, T_cal, tau, mean [n][2] (X @ beta), cur_pt [n][2] (log lambda, log mu), t3 [n][2]

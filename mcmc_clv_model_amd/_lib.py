@@ -115,6 +115,7 @@ def lib() -> ctypes.CDLL:
         "clv_debug_stamps": (c_int32, [sp, POINTER(c_uint64)]),
         "clv_debug_wg_stamps": (c_int32, [sp, POINTER(c_uint64)]),
         "clv_debug_exp": (c_int32, [dp, c_int64, dp]),
+        "clv_debug_log": (c_int32, [dp, c_int64, dp]),
         "clv_debug_mh_step": (c_int32, [c_int64, POINTER(c_int32), POINTER(c_uint8), dp, dp, dp, dp, dp,
                                         POINTER(c_float), dp, POINTER(c_float), dp]),
         "clv_debug_wg_map": (c_int32, [c_int32, c_int32, c_int32, POINTER(c_int32)]),

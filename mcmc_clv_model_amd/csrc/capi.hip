@@ -1241,17 +1241,22 @@ int clv_debug_mh_step(int64_t n, const int32_t* x, const uint8_t* z, const doubl
   return CLV_OK;
 }
 
-int clv_debug_exp(const double* x, int64_t n, double* out) {
+}  // extern "C"
+static int debug_fast_fn(const double* x, int64_t n, double* out, bool log_fn) {
   if (!x || !out || n < 1) return fail(CLV_EINVAL, "bad arguments");
   double *dx, *dout;
   CLV_HIP(dalloc(&dx, n));
   CLV_HIP(dalloc(&dout, n));
   CLV_HIP(hipMemcpy(dx, x, sizeof(double) * n, hipMemcpyHostToDevice));
-  CLV_HIP(launch_debug_exp(dx, n, dout, nullptr));
+  CLV_HIP(launch_debug_exp(dx, n, dout, nullptr, log_fn));
   CLV_HIP(hipMemcpy(out, dout, sizeof(double) * n, hipMemcpyDeviceToHost));
   CLV_HIP(hipFree(dx));
   CLV_HIP(hipFree(dout));
   return CLV_OK;
 }
+extern "C" {
+int clv_debug_exp(const double* x, int64_t n, double* out) { return debug_fast_fn(x, n, out, false); }
+
+int clv_debug_log(const double* x, int64_t n, double* out) { return debug_fast_fn(x, n, out, true); }
 
 }  // extern "C"

@@ -2,10 +2,11 @@
 //
 // exp(x) = 2^(k/256) * exp(r),  k = rint(x * 256/ln2) read from the low word of the "shifter"
 // sum x * 256/ln2 + 1.5 * 2^52,  r = x - k ln2/256 (Cody-Waite, two fma), |r| <= ln2/512;
-// 2^((k mod 256)/256) from a 256-entry LDS table (correctly rounded entries), scaled by 2^(k div
-// 256) with one integer add into its exponent field (no overflow/underflow for |x| <= 700);
-// expm1(r) by a degree-4 Taylor polynomial (truncation < r^5/120 ~ 3.7e-17 relative).
-// Error <= ~1 ulp, like ocml's exp; 11 VALU + 1 LDS read instead of ~20 VALU.
+// 2^((k mod 256)/256) from a 256-entry LDS table (correctly rounded entries); expm1(r) by a
+// degree-4 Taylor polynomial (truncation < r^5/120 ~ 3.7e-17 relative); the result
+// t + t expm1(r) scaled by 2^(k div 256) with v_ldexp_f64 (exact: no overflow/underflow for
+// |x| <= 700, the same bits as scaling t first).  Error <= ~1 ulp, like ocml's exp; 11 VALU +
+// 1 LDS read instead of ~20 VALU.
 // Constants: Python's decimal module at 80 digits, rounded to nearest (tools/gen_exp_table.py).
 #pragma once
 #include <hip/hip_runtime.h>
@@ -96,10 +97,8 @@ __device__ __forceinline__ double exp_fast(double x, const double* lds_tab) {
   p = __builtin_fma(p, r, 0.5);
   p = __builtin_fma(p, r, 1.0);
   p = p * r;                                             // expm1(r)
-  uint64_t tb = __builtin_bit_cast(uint64_t, lds_tab[ki & (EXP_TAB_N - 1)]);
-  tb += (uint64_t)(int64_t)(ki >> 8) << 52;              // * 2^(k div 256): exponent-field add
-  const double ts = __builtin_bit_cast(double, tb);
-  return __builtin_fma(ts, p, ts);
+  const double tab = lds_tab[ki & (EXP_TAB_N - 1)];
+  return __builtin_ldexp(__builtin_fma(tab, p, tab), ki >> 8);  // * 2^(k div 256) after the fma
 }
 
 // exp_fast of two independent arguments, bit-identical to two exp_fast calls, written so that both
@@ -124,12 +123,176 @@ __device__ __forceinline__ void exp_fast2(double x1, double x2, const double* ld
   p2 = __builtin_fma(p2, r2, 1.0);
   p1 = p1 * r1;
   p2 = p2 * r2;
-  uint64_t b1 = __builtin_bit_cast(uint64_t, tab1), b2 = __builtin_bit_cast(uint64_t, tab2);
-  b1 += (uint64_t)(int64_t)(ki1 >> 8) << 52;
-  b2 += (uint64_t)(int64_t)(ki2 >> 8) << 52;
-  const double s1 = __builtin_bit_cast(double, b1), s2 = __builtin_bit_cast(double, b2);
-  e1 = __builtin_fma(s1, p1, s1);
-  e2 = __builtin_fma(s2, p2, s2);
+  e1 = __builtin_ldexp(__builtin_fma(tab1, p1, tab1), ki1 >> 8);
+  e2 = __builtin_ldexp(__builtin_fma(tab2, p2, tab2), ki2 >> 8);
+}
+
+// ---- Fast fp64 log for x > 0 normal (the sampler's Philox-mode logs: lambda, mu, the dropout
+// time's uniform or truncated-exponential argument, eta's Box-Muller radius).  ocml's log is ~95
+// VALU (double-double reduction); this one is 19 VALU + one 16-byte LDS read, <= 1 ulp
+// (tools/gen_log_table.py: method, and a check against 60-digit logs with exact fma).
+//   x = 2^k z, z in [0.6865, 1.373) from the high word; bin i of z -> (invc, logc = -log invc);
+//   r = fma(z, invc, -1), |r| <= 2^-9;  log x = k ln2 + logc + log1p(r), log1p by its degree-6
+//   Taylor polynomial.  The bin around 1 has invc = 1, logc = 0: no cancellation near x = 1.
+// Table: LOG_TAB_N (invc, logc) pairs in LDS right after the exp table (FAST_TAB_N doubles).
+constexpr int LOG_TAB_N = 256;
+constexpr int FAST_TAB_N = EXP_TAB_N + 2 * LOG_TAB_N;
+constexpr uint32_t LOG_OFF_HI = 0x3fe5f800u;
+constexpr double LOG_LN2_HI = 0x1.62e42fefa3800p-1;
+constexpr double LOG_LN2_LO = 0x1.ef35793c76730p-45;
+__device__ constexpr double LOG_TAB[2 * LOG_TAB_N] = {  // (invc, logc) per bin
+    0x1.745d1745d1746p+0, -0x1.7fafa3bd8151cp-2, 0x1.734f0c541fe8dp+0, -0x1.7cc7f7db46a0ep-2,
+    0x1.724287f46debcp+0, -0x1.79e26687cfb3dp-2, 0x1.713786d9c7c09p+0, -0x1.76feecb947176p-2,
+    0x1.702e05c0b8170p+0, -0x1.741d876c67bb1p-2, 0x1.6f26016f26017p+0, -0x1.713e33a46a17cp-2,
+    0x1.6e1f76b4337c7p+0, -0x1.6e60ee6af1973p-2, 0x1.6d1a62681c861p+0, -0x1.6b85b4cffa3fdp-2,
+    0x1.6c16c16c16c17p+0, -0x1.68ac83e9c6a15p-2, 0x1.6b1490aa31a3dp+0, -0x1.65d558d4ce00bp-2,
+    0x1.6a13cd1537290p+0, -0x1.630030b3aac48p-2, 0x1.691473a88d0c0p+0, -0x1.602d08af091ecp-2,
+    0x1.6816816816817p+0, -0x1.5d5bddf595f31p-2, 0x1.6719f3601671ap+0, -0x1.5a8cadbbedfa1p-2,
+    0x1.661ec6a5122f9p+0, -0x1.57bf753c8d1fbp-2, 0x1.6524f853b4aa3p+0, -0x1.54f431b7be1a8p-2,
+    0x1.642c8590b2164p+0, -0x1.522ae0738a3d7p-2, 0x1.63356b88ac0dep+0, -0x1.4f637ebba9810p-2,
+    0x1.623fa77016240p+0, -0x1.4c9e09e172c3dp-2, 0x1.614b36831ae94p+0, -0x1.49da7f3bcc420p-2,
+    0x1.6058160581606p+0, -0x1.4718dc271c41cp-2, 0x1.5f66434292dfcp+0, -0x1.44591e0539f49p-2,
+    0x1.5e75bb8d015e7p+0, -0x1.419b423d5e8c6p-2, 0x1.5d867c3ece2a5p+0, -0x1.3edf463c1683ep-2,
+    0x1.5c9882b931057p+0, -0x1.3c25277333183p-2, 0x1.5babcc647fa91p+0, -0x1.396ce359bbf53p-2,
+    0x1.5ac056b015ac0p+0, -0x1.36b6776be1116p-2, 0x1.59d61f123ccaap+0, -0x1.3401e12aecba0p-2,
+    0x1.58ed2308158edp+0, -0x1.314f1e1d35ce3p-2, 0x1.5805601580560p+0, -0x1.2e9e2bce12286p-2,
+    0x1.571ed3c506b3ap+0, -0x1.2bef07cdc9355p-2, 0x1.56397ba7c52e2p+0, -0x1.2941afb186b7cp-2,
+    0x1.5555555555555p+0, -0x1.269621134db91p-2, 0x1.54725e6bb82fep+0, -0x1.23ec5991eba49p-2,
+    0x1.5390948f40febp+0, -0x1.214456d0eb8d5p-2, 0x1.52aff56a8054bp+0, -0x1.1e9e1678899f5p-2,
+    0x1.51d07eae2f815p+0, -0x1.1bf99635a6b95p-2, 0x1.50f22e111c4c5p+0, -0x1.1956d3b9bc2f9p-2,
+    0x1.5015015015015p+0, -0x1.16b5ccbacfb73p-2, 0x1.4f38f62dd4c9bp+0, -0x1.14167ef367784p-2,
+    0x1.4e5e0a72f0539p+0, -0x1.1178e8227e47ap-2, 0x1.4d843bedc2c4cp+0, -0x1.0edd060b78082p-2,
+    0x1.4cab88725af6ep+0, -0x1.0c42d676162e2p-2, 0x1.4bd3edda68fe1p+0, -0x1.09aa572e6c6d4p-2,
+    0x1.4afd6a052bf5bp+0, -0x1.07138604d5864p-2, 0x1.4a27fad76014ap+0, -0x1.047e60cde83b7p-2,
+    0x1.49539e3b2d067p+0, -0x1.01eae5626c691p-2, 0x1.4880522014880p+0, -0x1.feb2233ea07cbp-3,
+    0x1.47ae147ae147bp+0, -0x1.f991c6cb3b37ap-3, 0x1.46dce34596066p+0, -0x1.f474b134df228p-3,
+    0x1.460cbc7f5cf9ap+0, -0x1.ef5ade4dcffe5p-3, 0x1.453d9e2c776cap+0, -0x1.ea4449f04aaf5p-3,
+    0x1.446f86562d9fbp+0, -0x1.e530effe71013p-3, 0x1.43a2730abee4dp+0, -0x1.e020cc6235ab5p-3,
+    0x1.42d6625d51f87p+0, -0x1.db13db0d48941p-3, 0x1.420b5265e5951p+0, -0x1.d60a17f903514p-3,
+    0x1.4141414141414p+0, -0x1.d1037f2655e7bp-3, 0x1.40782d10e6566p+0, -0x1.cc000c9db3c52p-3,
+    0x1.3fb013fb013fbp+0, -0x1.c6ffbc6f00f71p-3, 0x1.3ee8f42a5af07p+0, -0x1.c2028ab17f9b5p-3,
+    0x1.3e22cbce4a902p+0, -0x1.bd087383bd8aap-3, 0x1.3d5d991aa75c6p+0, -0x1.b811730b823d4p-3,
+    0x1.3c995a47babe7p+0, -0x1.b31d8575bce3bp-3, 0x1.3bd60d9232955p+0, -0x1.ae2ca6f672bd8p-3,
+    0x1.3b13b13b13b14p+0, -0x1.a93ed3c8ad9e5p-3, 0x1.3a524387ac822p+0, -0x1.a454082e6ab03p-3,
+    0x1.3991c2c187f63p+0, -0x1.9f6c407089663p-3, 0x1.38d22d366088ep+0, -0x1.9a8778debaa3ap-3,
+    0x1.3813813813814p+0, -0x1.95a5adcf70182p-3, 0x1.3755bd1c945eep+0, -0x1.90c6db9fcbcdbp-3,
+    0x1.3698df3de0748p+0, -0x1.8beafeb38fe8fp-3, 0x1.35dce5f9f2af8p+0, -0x1.871213750e994p-3,
+    0x1.3521cfb2b78c1p+0, -0x1.823c16551a3c0p-3, 0x1.34679ace01346p+0, -0x1.7d6903caf5acdp-3,
+    0x1.33ae45b57bcb2p+0, -0x1.7898d85444c74p-3, 0x1.32f5ced6a1dfap+0, -0x1.73cb9074fd14dp-3,
+    0x1.323e34a2b10bfp+0, -0x1.6f0128b756ab9p-3, 0x1.3187758e9ebb6p+0, -0x1.6a399dabbd383p-3,
+    0x1.30d190130d190p+0, -0x1.6574ebe8c1339p-3, 0x1.301c82ac40260p+0, -0x1.60b3100b09474p-3,
+    0x1.2f684bda12f68p+0, -0x1.5bf406b543db0p-3, 0x1.2eb4ea1fed14bp+0, -0x1.5737cc9018cddp-3,
+    0x1.2e025c04b8097p+0, -0x1.527e5e4a1b58dp-3, 0x1.2d50a012d50a0p+0, -0x1.4dc7b897bc1c7p-3,
+    0x1.2c9fb4d812ca0p+0, -0x1.4913d8333b563p-3, 0x1.2bef98e5a3711p+0, -0x1.4462b9dc9b3dcp-3,
+    0x1.2b404ad012b40p+0, -0x1.3fb45a59928cap-3, 0x1.2a91c92f3c105p+0, -0x1.3b08b6757f2a7p-3,
+    0x1.29e4129e4129ep+0, -0x1.365fcb0159014p-3, 0x1.293725bb804a5p+0, -0x1.31b994d3a4f86p-3,
+    0x1.288b01288b013p+0, -0x1.2d1610c86813dp-3, 0x1.27dfa38a1ce4dp+0, -0x1.28753bc11aba2p-3,
+    0x1.27350b8812735p+0, -0x1.23d712a49c201p-3, 0x1.268b37cd60127p+0, -0x1.1f3b925f25d44p-3,
+    0x1.25e22708092f1p+0, -0x1.1aa2b7e23f729p-3, 0x1.2539d7e9177b2p+0, -0x1.160c8024b27b0p-3,
+    0x1.2492492492492p+0, -0x1.1178e8227e47ap-3, 0x1.23eb79717605bp+0, -0x1.0ce7ecdccc28bp-3,
+    0x1.23456789abcdfp+0, -0x1.08598b59e3a07p-3, 0x1.22a0122a0122ap+0, -0x1.03cdc0a51ec0dp-3,
+    0x1.21fb78121fb78p+0, -0x1.fe89139dbd565p-4, 0x1.21579804855e6p+0, -0x1.f57bc7d9005dbp-4,
+    0x1.20b470c67c0d9p+0, -0x1.ec739830a1126p-4, 0x1.2012012012012p+0, -0x1.e3707ee30487bp-4,
+    0x1.1f7047dc11f70p+0, -0x1.da7276384469ep-4, 0x1.1ecf43c7fb84cp+0, -0x1.d179788219362p-4,
+    0x1.1e2ef3b3fb874p+0, -0x1.c885801bc4b20p-4, 0x1.1d8f5672e4abdp+0, -0x1.bf968769fca18p-4,
+    0x1.1cf06ada2811dp+0, -0x1.b6ac88dad5b1dp-4, 0x1.1c522fc1ce059p+0, -0x1.adc77ee5aea8ep-4,
+    0x1.1bb4a4046ed29p+0, -0x1.a4e7640b1bc38p-4, 0x1.1b17c67f2bae3p+0, -0x1.9c0c32d4d254dp-4,
+    0x1.1a7b9611a7b96p+0, -0x1.9335e5d594988p-4, 0x1.19e0119e0119ep+0, -0x1.8a6477a91dc29p-4,
+    0x1.19453808ca29cp+0, -0x1.8197e2f40e3f0p-4, 0x1.18ab083902bdbp+0, -0x1.78d02263d82d7p-4,
+    0x1.1811811811812p+0, -0x1.700d30aeac0e8p-4, 0x1.1778a191bd684p+0, -0x1.674f089365a78p-4,
+    0x1.16e0689427379p+0, -0x1.5e95a4d9791cdp-4, 0x1.1648d50fc3201p+0, -0x1.55e10050e0382p-4,
+    0x1.15b1e5f75270dp+0, -0x1.4d3115d207eacp-4, 0x1.151b9a3fdd5c9p+0, -0x1.4485e03dbdfb0p-4,
+    0x1.1485f0e0acd3bp+0, -0x1.3bdf5a7d1ee5ep-4, 0x1.13f0e8d344724p+0, -0x1.333d7f8183f4ap-4,
+    0x1.135c81135c811p+0, -0x1.2aa04a44717a1p-4, 0x1.12c8b89edc0acp+0, -0x1.2207b5c7854a1p-4,
+    0x1.12358e75d3033p+0, -0x1.1973bd1465561p-4, 0x1.11a3019a74826p+0, -0x1.10e45b3cae829p-4,
+    0x1.1111111111111p+0, -0x1.08598b59e3a06p-4, 0x1.107fbbe011080p+0, -0x1.ffa6911ab9309p-5,
+    0x1.0fef010fef011p+0, -0x1.eea31c006b87cp-5, 0x1.0f5edfab325a2p+0, -0x1.dda8adc67ee59p-5,
+    0x1.0ecf56be69c90p+0, -0x1.ccb73cdddb2d0p-5, 0x1.0e40655826011p+0, -0x1.bbcebfc68f424p-5,
+    0x1.0db20a88f4696p+0, -0x1.aaef2d0fb1108p-5, 0x1.0d24456359e3ap+0, -0x1.9a187b573de81p-5,
+    0x1.0c9714fbcda3bp+0, -0x1.894aa149fb34bp-5, 0x1.0c0a7868b4171p+0, -0x1.788595a3577c8p-5,
+    0x1.0b7e6ec259dc8p+0, -0x1.67c94f2d4bb65p-5, 0x1.0af2f722eecb5p+0, -0x1.5715c4c03cee1p-5,
+    0x1.0a6810a6810a7p+0, -0x1.466aed42de3f9p-5, 0x1.09ddba6af8360p+0, -0x1.35c8bfaa13069p-5,
+    0x1.0953f39010954p+0, -0x1.252f32f8d1840p-5, 0x1.08cabb37565e2p+0, -0x1.149e3e4005a8dp-5,
+    0x1.0842108421084p+0, -0x1.0415d89e74440p-5, 0x1.07b9f29b8eae2p+0, -0x1.e72bf2813ce6ap-6,
+    0x1.073260a47f7c6p+0, -0x1.c63d2ec14aad7p-6, 0x1.06ab59c7912fbp+0, -0x1.a55f548c5c427p-6,
+    0x1.0624dd2f1a9fcp+0, -0x1.8492528c8cac5p-6, 0x1.059eea0727586p+0, -0x1.63d6178690bbep-6,
+    0x1.05197f7d73404p+0, -0x1.432a925980cbcp-6, 0x1.04949cc1664c5p+0, -0x1.228fb1fea2e0ap-6,
+    0x1.0410410410410p+0, -0x1.0205658935837p-6, 0x1.038c6b78247fcp+0, -0x1.c317384c75f0dp-7,
+    0x1.03091b51f5e1ap+0, -0x1.82448a388a283p-7, 0x1.02864fc7729e9p+0, -0x1.41929f968330cp-7,
+    0x1.0204081020408p+0, -0x1.010157588de69p-7, 0x1.0182436517a37p+0, -0x1.8121214586b02p-8,
+    0x1.0101010101010p+0, -0x1.0080559588b25p-8, 0x1.0080402010080p+0, -0x1.0040155d5881ep-9,
+    0x1.0000000000000p+0, 0x0.0p+0, 0x1.fe01fe01fe020p-1, 0x1.ff00aa2b10ba0p-9,
+    0x1.fc07f01fc07f0p-1, 0x1.fe02a6b106799p-8, 0x1.fa11caa01fa12p-1, 0x1.7dc475f810a69p-7,
+    0x1.f81f81f81f820p-1, 0x1.fc0a8b0fc03c4p-7, 0x1.f6310aca0dbb5p-1, 0x1.3cea44346a584p-6,
+    0x1.f44659e4a4271p-1, 0x1.7b91b07d5b126p-6, 0x1.f25f644230ab5p-1, 0x1.b9fc027af919ap-6,
+    0x1.f07c1f07c1f08p-1, 0x1.f829b0e7832f8p-6, 0x1.ee9c7f8458e02p-1, 0x1.1b0d98923d97fp-5,
+    0x1.ecc07b301ecc0p-1, 0x1.39e87b9febd68p-5, 0x1.eae807aba01ebp-1, 0x1.58a5bafc8e4d3p-5,
+    0x1.e9131abf0b767p-1, 0x1.77458f632dcffp-5, 0x1.e741aa59750e4p-1, 0x1.95c830ec8e3f2p-5,
+    0x1.e573ac901e574p-1, 0x1.b42dd711971b9p-5, 0x1.e3a9179dc1a73p-1, 0x1.d276b8adb0b56p-5,
+    0x1.e1e1e1e1e1e1ep-1, 0x1.f0a30c01162a8p-5, 0x1.e01e01e01e01ep-1, 0x1.075983598e471p-4,
+    0x1.de5d6e3f8868ap-1, 0x1.16536eea37ae3p-4, 0x1.dca01dca01dcap-1, 0x1.253f62f0a1417p-4,
+    0x1.dae6076b981dbp-1, 0x1.341d7961bd1d0p-4, 0x1.d92f2231e7f8ap-1, 0x1.42edcbea646eep-4,
+    0x1.d77b654b82c34p-1, 0x1.51b073f06183cp-4, 0x1.d5cac807572b2p-1, 0x1.60658a93750c4p-4,
+    0x1.d41d41d41d41dp-1, 0x1.6f0d28ae56b4ep-4, 0x1.d272ca3fc5b1ap-1, 0x1.7da766d7b12d0p-4,
+    0x1.d0cb58f6ec074p-1, 0x1.8c345d6319b23p-4, 0x1.cf26e5c44bfc6p-1, 0x1.9ab42462033aep-4,
+    0x1.cd85689039b0bp-1, 0x1.a926d3a4ad562p-4, 0x1.cbe6d9601cbe7p-1, 0x1.b78c82bb0eda0p-4,
+    0x1.ca4b3055ee191p-1, 0x1.c5e548f5bc743p-4, 0x1.c8b265afb8a42p-1, 0x1.d4313d66cb35dp-4,
+    0x1.c71c71c71c71cp-1, 0x1.e27076e2af2eap-4, 0x1.c5894d10d4986p-1, 0x1.f0a30c01162a4p-4,
+    0x1.c3f8f01c3f8f0p-1, 0x1.fec9131dbeabcp-4, 0x1.c26b5392ea01cp-1, 0x1.0671512ca596fp-3,
+    0x1.c0e070381c0e0p-1, 0x1.0d77e7cd08e5bp-3, 0x1.bf583ee868d8bp-1, 0x1.14785846742acp-3,
+    0x1.bdd2b899406f7p-1, 0x1.1b72ad52f67a2p-3, 0x1.bc4fd65883e7bp-1, 0x1.2266f190a5acdp-3,
+    0x1.bacf914c1bad0p-1, 0x1.29552f81ff521p-3, 0x1.b951e2b18ff23p-1, 0x1.303d718e47fd5p-3,
+    0x1.b7d6c3dda338bp-1, 0x1.371fc201e8f75p-3, 0x1.b65e2e3beee05p-1, 0x1.3dfc2b0ecc62ap-3,
+    0x1.b4e81b4e81b4fp-1, 0x1.44d2b6ccb7d1cp-3, 0x1.b37484ad806cep-1, 0x1.4ba36f39a55e5p-3,
+    0x1.b2036406c80d9p-1, 0x1.526e5e3a1b438p-3, 0x1.b094b31d922a4p-1, 0x1.59338d9982085p-3,
+    0x1.af286bca1af28p-1, 0x1.5ff3070a793d6p-3, 0x1.adbe87f94905ep-1, 0x1.66acd4272ad51p-3,
+    0x1.ac5701ac5701bp-1, 0x1.6d60fe719d21bp-3, 0x1.aaf1d2f87ebfdp-1, 0x1.740f8f54037a3p-3,
+    0x1.a98ef606a63bep-1, 0x1.7ab890210d907p-3, 0x1.a82e65130e159p-1, 0x1.815c0a14357e9p-3,
+    0x1.a6d01a6d01a6dp-1, 0x1.87fa06520c911p-3, 0x1.a574107688a4ap-1, 0x1.8e928de886d41p-3,
+    0x1.a41a41a41a41ap-1, 0x1.9525a9cf456b6p-3, 0x1.a2c2a87c51ca0p-1, 0x1.9bb362e7dfb85p-3,
+    0x1.a16d3f97a4b02p-1, 0x1.a23bc1fe2b561p-3, 0x1.a01a01a01a01ap-1, 0x1.a8becfc882f19p-3,
+    0x1.9ec8e951033d9p-1, 0x1.af3c94e80bff3p-3, 0x1.9d79f176b682dp-1, 0x1.b5b519e8fb5a6p-3,
+    0x1.9c2d14ee4a102p-1, 0x1.bc286742d8cd4p-3, 0x1.9ae24ea5510dap-1, 0x1.c2968558c18c2p-3,
+    0x1.999999999999ap-1, 0x1.c8ff7c79a9a20p-3, 0x1.9852f0d8ec0ffp-1, 0x1.cf6354e09c5ddp-3,
+    0x1.970e4f80cb872p-1, 0x1.d5c216b4fbb94p-3, 0x1.95cbb0be377aep-1, 0x1.dc1bca0abec7bp-3,
+    0x1.948b0fcd6e9e0p-1, 0x1.e27076e2af2e8p-3, 0x1.934c67f9b2ce6p-1, 0x1.e8c0252aa5a60p-3,
+    0x1.920fb49d0e229p-1, 0x1.ef0adcbdc5935p-3, 0x1.90d4f120190d5p-1, 0x1.f550a564b7b37p-3,
+    0x1.8f9c18f9c18fap-1, 0x1.fb9186d5e3e29p-3, 0x1.8e6527af1373fp-1, 0x1.00e6c45ad501dp-2,
+    0x1.8d3018d3018d3p-1, 0x1.0402594b4d041p-2, 0x1.8bfce8062ff3ap-1, 0x1.071b85fcd590dp-2,
+    0x1.8acb90f6bf3aap-1, 0x1.0a324e27390e2p-2, 0x1.899c0f601899cp-1, 0x1.0d46b579ab74bp-2,
+    0x1.886e5f0abb04ap-1, 0x1.1058bf9ae4ad4p-2, 0x1.87427bcc092b9p-1, 0x1.136870293a8b0p-2,
+    0x1.8618618618618p-1, 0x1.1675cababa60fp-2, 0x1.84f00c2780614p-1, 0x1.1980d2dd4236fp-2,
+    0x1.83c977ab2beddp-1, 0x1.1c898c16999fbp-2, 0x1.82a4a0182a4a0p-1, 0x1.1f8ff9e48a2f3p-2,
+    0x1.8181818181818p-1, 0x1.22941fbcf7966p-2, 0x1.8060180601806p-1, 0x1.2596010df763ap-2,
+    0x1.7f405fd017f40p-1, 0x1.2895a13de86a4p-2, 0x1.7e225515a4f1dp-1, 0x1.2b9303ab89d25p-2,
+    0x1.7d05f417d05f4p-1, 0x1.2e8e2bae11d31p-2, 0x1.7beb3922e017cp-1, 0x1.31871c9544185p-2,
+    0x1.7ad2208e0ecc3p-1, 0x1.347dd9a987d56p-2, 0x1.79baa6bb6398bp-1, 0x1.3772662bfd85cp-2,
+    0x1.78a4c8178a4c8p-1, 0x1.3a64c556945eap-2, 0x1.77908119ac60dp-1, 0x1.3d54fa5c1f710p-2,
+    0x1.767dce434a9b1p-1, 0x1.404308686a7e4p-2, 0x1.756cac201756dp-1, 0x1.432ef2a04e813p-2,
+};
+
+__device__ __forceinline__ double log_fast(double x, const double* lds_tab) {
+  const uint64_t ix = __builtin_bit_cast(uint64_t, x);
+  const uint32_t h = (uint32_t)(ix >> 32);
+  const uint32_t t = h - LOG_OFF_HI;
+  const int k = (int)t >> 20;
+  const uint32_t i = (t >> 12) & (LOG_TAB_N - 1);
+  const double z = __builtin_bit_cast(double, ((uint64_t)(h - (t & 0xfff00000u)) << 32) | (uint32_t)ix);
+  const double2 e = reinterpret_cast<const double2*>(lds_tab + EXP_TAB_N)[i];  // (invc, logc)
+  const double r = __builtin_fma(z, e.x, -1.0);
+  const double kd = (double)k;
+  double p = __builtin_fma(r, -1.0 / 6.0, 1.0 / 5.0);
+  p = __builtin_fma(p, r, -1.0 / 4.0);
+  p = __builtin_fma(p, r, 1.0 / 3.0);
+  p = __builtin_fma(p, r, -0.5);
+  const double lp = __builtin_fma(r * r, p, r);  // log1p(r)
+  return __builtin_fma(kd, LOG_LN2_HI, e.y) + __builtin_fma(kd, LOG_LN2_LO, lp);
+}
+
+// Fills the LDS table of exp_fast / log_fast (FAST_TAB_N doubles) from nt threads.
+__device__ __forceinline__ void fast_tab_fill(double* lds_tab, int tid, int nt) {
+  for (int j = tid; j < EXP_TAB_N; j += nt) lds_tab[j] = EXP2_TAB[j];
+  for (int j = tid; j < 2 * LOG_TAB_N; j += nt) lds_tab[EXP_TAB_N + j] = LOG_TAB[j];
 }
 
 }  // namespace clv

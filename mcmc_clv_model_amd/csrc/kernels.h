@@ -148,7 +148,7 @@ hipError_t launch_debug_level2(int D, int K, const double* prior_dev, const doub
                                hipStream_t st);
 hipError_t launch_debug_hyper_variates(uint64_t seed, int chain, uint32_t sweep, double df, int64_t n,
                                        double* chi2, double* normals, hipStream_t st);
-hipError_t launch_debug_exp(const double* x, int64_t n, double* out, hipStream_t st);
+hipError_t launch_debug_exp(const double* x, int64_t n, double* out, hipStream_t st, bool log_fn = false);
 hipError_t launch_debug_mh(const int32_t* x, const uint8_t* z, const double* T, const double* tau, const double* m,
                            const double* prec, const double* cur_pt, const float* t3, const double* scale,
                            const float* log_u, int64_t n, double* out, hipStream_t st);

@@ -1056,36 +1056,49 @@ __device__ __forceinline__ void cust_ztau(Cust<D, K, CL>& u, const SweepArgs& a,
   // Philox mode: exp_fast, argument capped at 700 (exp(-700) ~ 1e-304 already makes
   // p(alive) < 2^-53, the smallest nonzero u_z, as exp(-zz) underflowing to 0 does)
   const double e = REPLAY ? exp(-zz) : exp_fast(-min700(zz), exp_tab);
-  const double p = (ml * e) / (ml * e + mu * (1.0 - e));
-  const bool z = u_z < p;
+  bool z;
+  if constexpr (REPLAY) {
+    const double p = (ml * e) / (ml * e + mu * (1.0 - e));
+    z = u_z < p;
+  } else {  // Philox mode: u_z < a / b as u_z * b < a (b > 0), no fp64 division
+    const double ae = ml * e;
+    z = u_z * (ae + mu * (1.0 - e)) < ae;
+  }
   u.z = z;
 
   // ---- draw_tau (bi:203-227)
   double tau;
-  if (z) {
-    double E;
-    if constexpr (REPLAY) E = v_tau; else E = -log(u53_open0(rz, rw));
-    tau = T + (1.0 / mu) * E;
-  } else {
-    double uu;
-    if constexpr (REPLAY) uu = v_tau; else uu = u53(rz, rw);
-    const double ml_tx = min700(ml * tx);
-    const double ml_T = min700(ml * T);
-    double e_tx, e_T;  // both capped at 700 (bi:223)
-    if constexpr (REPLAY) {
-      e_tx = exp(-ml_tx);
-      e_T = exp(-ml_T);
+  if constexpr (REPLAY) {
+    if (z) {
+      tau = T + (1.0 / mu) * v_tau;
     } else {
-      exp_fast2(-ml_tx, -ml_T, exp_tab, e_tx, e_T);
+      const double uu = v_tau;
+      const double e_tx = exp(-min700(ml * tx));  // both capped at 700 (bi:223)
+      const double e_T = exp(-min700(ml * T));
+      tau = -log((1 - uu) * e_tx + uu * e_T) / ml;
     }
-    tau = -log((1 - uu) * e_tx + uu * e_T) / ml;
+  } else {
+    // Philox mode, branch-free (the lanes of a wave mix alive and churned customers): one
+    // log_fast of either -E's uniform U' in (0, 1] (alive: tau = T + E / mu) or the truncated
+    // exponential's argument (churned: tau = -log(.) / ml), one division
+    const double uu = u53(rz, rw);
+    double e_tx, e_T;
+    exp_fast2(-min700(ml * tx), -min700(ml * T), exp_tab, e_tx, e_T);
+    const double L = log_fast(z ? u53_open0(rz, rw) : (1 - uu) * e_tx + uu * e_T, exp_tab);
+    const double q = L / (z ? mu : ml);
+    tau = z ? T - q : -q;
   }
   u.tau = tau;
   u.lc.xm = u.xm;
   u.lc.omz = z ? 0.0 : 1.0;
   u.lc.w = z ? T : tau;
-  u.ll = log(lam);
-  u.lm = log(mu);
+  if constexpr (REPLAY) {
+    u.ll = log(lam);
+    u.lm = log(mu);
+  } else {
+    u.ll = log_fast(lam, exp_tab);
+    u.lm = log_fast(mu, exp_tab);
+  }
 }
 
 // Phase A2b (bi:280-290): log-posterior constants from (beta, Sigma) and the current point's
@@ -1144,12 +1157,22 @@ __device__ __forceinline__ double clip70_fma(double a, double b, double c) {
 // pm <= 5 and exp(plp - cur) > u  <=>  plp > cur + log(u)  (cur = -inf accepts any finite one;
 // cur + log u is formed off the dependent chain, alongside the proposal; a padded step's
 // log u = +inf gives +inf or NaN there, never accepted).
+// The log mu proposal needs only the lower bound: a proposal above 5 is rejected by the Q3 cap
+// whatever its value (and its log posterior, even NaN, is then never looked at), and an accepted
+// one is <= 5 < 70, so max(., -70) accepts exactly what clip(., -70, 70) does.
+__device__ __forceinline__ double prop_lm(double a, double b, double c) {
+  double r, lo = -70.0;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(r), "s"(lo));
+  return r;
+}
+
 template <int D, int K, bool CL>
 __device__ __forceinline__ void mh_step(Cust<D, K, CL>& u, double s00, double s11, float t_l, float t_m, float l_u,
                                         const double* exp_tab) {
   const double thr = u.cur + (double)l_u;
   const double pl = clip70_fma(s00, (double)t_l, u.ll);
-  const double pm = clip70_fma(s11, (double)t_m, u.lm);
+  const double pm = prop_lm(s11, (double)t_m, u.lm);
   const double plp = log_post_fast(u.fc, pl, pm, exp_tab);
   // selects, not a branch: keeps a chunk's steps in one basic block with the next chunk's variates
   const bool acc = (pm <= 5.0) & (plp > thr);
@@ -1258,9 +1281,9 @@ struct CustOut {
 // draw_eta's standard normal (tri:333 rng.normal), Philox mode: fp64 Box-Muller from the
 // customer's SLOT_ETA block.  Independent of the state, so the persistent kernel draws it for
 // sweep s+1 in the level-2 hand-off window (with the MH variates), off the sweep's serial path.
-__device__ __forceinline__ double eta_normal(uint32_t k0, uint32_t k1, uint32_t gi, int64_t s) {
+__device__ __forceinline__ double eta_normal(uint32_t k0, uint32_t k1, uint32_t gi, int64_t s, const double* tab) {
   const u32x4 r = customer_block(k0, k1, gi, (uint32_t)s, SLOT_ETA);
-  return sqrt(-2.0 * log(u53_open0(r.x, r.y))) * cospi(2.0 * u53(r.z, r.w));
+  return sqrt(-2.0 * log_fast(u53_open0(r.x, r.y), tab)) * cospi(2.0 * u53(r.z, r.w));
 }
 
 template <int D, int K, bool REPLAY, bool CL>
@@ -1290,7 +1313,7 @@ __device__ __forceinline__ CustOut<D> cust_finish(Cust<D, K, CL>& u, const Sweep
     if constexpr (REPLAY) {
       zeta = tape[(int64_t)(2 + 3 * g.S) * g.n + i];
     } else {
-      zeta = zeta_pre ? *zeta_pre : eta_normal(k0, k1, u.gi, s);
+      zeta = zeta_pre ? *zeta_pre : eta_normal(k0, k1, u.gi, s, exp_tab);
     }
     const double xe = post_mean + H[H_SQRT_POSTVAR] * zeta;
     if constexpr (REPLAY) {
@@ -1390,11 +1413,16 @@ __device__ __forceinline__ void sweep_body(const SweepArgs& a) {
   constexpr int NS = NXY + NYY + 1;
   __shared__ double red[BLOCK / 64][NS];
   __shared__ double tot[NS];
-  __shared__ double exp_tab[EXP_TAB_N];
-  // the exp table's global load is issued first; it is stored to LDS (and the barrier taken)
-  // after the customer's own loads are in flight
-  double tab_v = 0.0;
-  if (!REPLAY) tab_v = EXP2_TAB[threadIdx.x];  // BLOCK == EXP_TAB_N
+  __shared__ __attribute__((aligned(16))) double exp_tab[FAST_TAB_N];
+  // the exp/log table's global loads are issued first; they are stored to LDS (and the barrier
+  // taken) after the customer's own loads are in flight
+  static_assert(BLOCK == EXP_TAB_N && BLOCK == LOG_TAB_N, "one table entry per thread");
+  double tab_v = 0.0, tab_l0 = 0.0, tab_l1 = 0.0;
+  if (!REPLAY) {
+    tab_v = EXP2_TAB[threadIdx.x];
+    tab_l0 = LOG_TAB[2 * threadIdx.x];
+    tab_l1 = LOG_TAB[2 * threadIdx.x + 1];
+  }
 
   const Geometry& g = a.g;
   const int c = blockIdx.y;
@@ -1451,7 +1479,11 @@ __device__ __forceinline__ void sweep_body(const SweepArgs& a) {
       a.mu[ci] = mu;
     }
   }
-  if (!REPLAY) exp_tab[threadIdx.x] = tab_v;
+  if (!REPLAY) {
+    exp_tab[threadIdx.x] = tab_v;
+    exp_tab[EXP_TAB_N + 2 * threadIdx.x] = tab_l0;
+    exp_tab[EXP_TAB_N + 2 * threadIdx.x + 1] = tab_l1;
+  }
   __syncthreads();
   if (threadIdx.x == 0 && !a.init) CLV_WG_STAMP(a.stamps, (int64_t)c * g.nb_local + b, 8);
 
@@ -2013,7 +2045,7 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
   constexpr int NTRIL = D * (D - 1) / 2;
   __shared__ double red[BLOCK / 64][NS];
   __shared__ double tot[NS];
-  __shared__ double exp_tab[EXP_TAB_N];
+  __shared__ __attribute__((aligned(16))) double exp_tab[FAST_TAB_N];
   __shared__ double Hs[HS];
   __shared__ uint32_t s_abort;
   // customer workgroups: the drawn-ahead MH variates; the level-2 workgroup (P2P): its unit partials
@@ -2050,7 +2082,7 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
     cu.i = cu.active ? i : (g.n > 0 ? g.n - 1 : 0);
   }
   cust_load(cu, a, c);  // once per launch: CBS row, covariates, state stay in registers
-  exp_tab[tid] = EXP2_TAB[tid];
+  fast_tab_fill(exp_tab, tid, BLOCK);
   if (tid < HS) Hs[tid] = a.hyper[(int64_t)c * HS + tid];  // sweep s_first: from before this launch
   __syncthreads();
   if (cu.active) cust_ztau<D, K, false>(cu, a, s_first, k0, k1, nullptr, exp_tab);
@@ -2059,7 +2091,7 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
   const PreVariates pv{(float2*)pool, (float*)(pool + PRE_STEPS * BLOCK * 8), tid};
   if (cu.active && pre) mh_pre_variates(SlotPhilox(k0, k1, cu.gi, (uint32_t)s_first), g.S, pv);
   if constexpr (D == 3) {
-    if (cu.active && pre) zeta_lds[tid] = eta_normal(k0, k1, cu.gi, s_first);
+    if (cu.active && pre) zeta_lds[tid] = eta_normal(k0, k1, cu.gi, s_first, exp_tab);
   }
   const double* hyp_c = a.hyp2 + (int64_t)c * HS;
   for (int64_t it = 0; it < n_sweeps; ++it) {
@@ -2103,7 +2135,7 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
       else mh_run(cu, SlotPhilox(k0, k1, cu.gi, (uint32_t)s), s00, s11, g.S, exp_tab);
       CLV_P_STAMP(a.stamps, wgi, 3, stp);
       if constexpr (D == 3) {
-        if (!pre) zeta_lds[tid] = eta_normal(k0, k1, cu.gi, s);  // (not drawn ahead: S > PRE_STEPS)
+        if (!pre) zeta_lds[tid] = eta_normal(k0, k1, cu.gi, s, exp_tab);  // (not drawn ahead: S > PRE_STEPS)
       }
       out = cust_finish<D, K, false>(cu, a, s, stored, Hs, k0, k1, nullptr, exp_tab, st,
                                      D == 3 ? &zeta_lds[tid] : nullptr);
@@ -2132,7 +2164,7 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
         cust_ztau<D, K, false>(cu, a, s + 1, k0, k1, nullptr, exp_tab);
         if (pre) mh_pre_variates(SlotPhilox(k0, k1, cu.gi, (uint32_t)(s + 1)), g.S, pv);
         if constexpr (D == 3) {
-          if (pre) zeta_lds[tid] = eta_normal(k0, k1, cu.gi, s + 1);
+          if (pre) zeta_lds[tid] = eta_normal(k0, k1, cu.gi, s + 1, exp_tab);
         }
       }
     }
@@ -2172,6 +2204,9 @@ __global__ void debug_philox_kernel(uint32_t k0, uint32_t k1, const uint32_t* ct
 
 __global__ void debug_variates_kernel(uint64_t seed, int chain, uint32_t sweep, int64_t n, int S, float* tl,
                                       float* tm, float* ua, double* uz, double* ut, double* ea, double* ez) {
+  __shared__ __attribute__((aligned(16))) double tab[FAST_TAB_N];
+  fast_tab_fill(tab, threadIdx.x, blockDim.x);
+  __syncthreads();
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t k0, k1;
@@ -2179,9 +2214,8 @@ __global__ void debug_variates_kernel(uint64_t seed, int chain, uint32_t sweep, 
   const u32x4 r = customer_block(k0, k1, (uint32_t)i, sweep, SLOT_ZTAU);
   uz[i] = u53(r.x, r.y);
   ut[i] = u53(r.z, r.w);
-  ea[i] = -log(u53_open0(r.z, r.w));
-  const u32x4 re = customer_block(k0, k1, (uint32_t)i, sweep, SLOT_ETA);
-  ez[i] = sqrt(-2.0 * log(u53_open0(re.x, re.y))) * cospi(2.0 * u53(re.z, re.w));
+  ea[i] = -log_fast(u53_open0(r.z, r.w), tab);  // as cust_ztau's alive dropout time
+  ez[i] = eta_normal(k0, k1, (uint32_t)i, sweep, tab);
   const SlotPhilox ph(k0, k1, (uint32_t)i, sweep);
   for (int j = 0; j < S; ++j) {
     const u32x4 r = ph(SLOT_MH0 + (uint32_t)j);
@@ -2226,12 +2260,13 @@ __global__ void debug_hyper_variates_kernel(uint64_t seed, int chain, uint32_t s
   normals[i] = hyper_normal(k0, k1, HSLOT_NORMAL0, sweep + (uint32_t)i);
 }
 
+template <bool LOG>
 __global__ void debug_exp_kernel(const double* x, int64_t n, double* out) {
-  __shared__ double tab[EXP_TAB_N];
-  for (int j = threadIdx.x; j < EXP_TAB_N; j += blockDim.x) tab[j] = EXP2_TAB[j];
+  __shared__ __attribute__((aligned(16))) double tab[FAST_TAB_N];
+  fast_tab_fill(tab, threadIdx.x, blockDim.x);
   __syncthreads();
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) out[i] = exp_fast(x[i], tab);
+  if (i < n) out[i] = LOG ? log_fast(x[i], tab) : exp_fast(x[i], tab);
 }
 
 // The shipped Philox-mode MH step on given inputs (tests only): per lane, the log-posterior
@@ -2243,8 +2278,8 @@ __global__ void debug_exp_kernel(const double* x, int64_t n, double* out) {
 __global__ void debug_mh_kernel(const int32_t* x, const uint8_t* z, const double* T, const double* tau,
                                 const double* m, const double* prec, const double* cur_pt, const float* t3,
                                 const double* scale, const float* log_u, int64_t n, double* out) {
-  __shared__ double tab[EXP_TAB_N];
-  for (int j = threadIdx.x; j < EXP_TAB_N; j += blockDim.x) tab[j] = EXP2_TAB[j];
+  __shared__ __attribute__((aligned(16))) double tab[FAST_TAB_N];
+  fast_tab_fill(tab, threadIdx.x, blockDim.x);
   __syncthreads();
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -2267,7 +2302,7 @@ __global__ void debug_mh_kernel(const int32_t* x, const uint8_t* z, const double
   cust_coeffs<2, 1, false>(u, H, tab);
   const double cur0 = u.cur;
   const double pl = clip70_fma(scale[0], (double)t3[2 * i], u.ll);
-  const double pm = clip70_fma(scale[1], (double)t3[2 * i + 1], u.lm);
+  const double pm = prop_lm(scale[1], (double)t3[2 * i + 1], u.lm);
   const double plp = log_post_fast(u.fc, pl, pm, tab);
   mh_step(u, scale[0], scale[1], t3[2 * i], t3[2 * i + 1], log_u[i], tab);
   double* o = out + 7 * i;
@@ -2394,8 +2429,9 @@ hipError_t launch_debug_hyper_variates(uint64_t seed, int chain, uint32_t sweep,
   return hipGetLastError();
 }
 
-hipError_t launch_debug_exp(const double* x, int64_t n, double* out, hipStream_t st) {
-  hipLaunchKernelGGL(debug_exp_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, n, out);
+hipError_t launch_debug_exp(const double* x, int64_t n, double* out, hipStream_t st, bool log_fn) {
+  if (log_fn) hipLaunchKernelGGL(debug_exp_kernel<true>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, n, out);
+  else hipLaunchKernelGGL(debug_exp_kernel<false>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, n, out);
   return hipGetLastError();
 }
 

@@ -134,7 +134,7 @@ __device__ __forceinline__ float ln_f32(float u) {  // natural log via v_log_f32
 // a symmetric lattice of angles, so the proposal stays symmetric and MH stays exact.
 __device__ __forceinline__ float t3_f32(float u, float v) {
   const float p = __builtin_amdgcn_exp2f(-(2.0f / 3.0f) * __builtin_amdgcn_logf(u));  // U^(-2/3)
-  const float r = __builtin_amdgcn_sqrtf(3.0f * (p - 1.0f));
+  const float r = __builtin_amdgcn_sqrtf(__builtin_fmaf(3.0f, p, -3.0f));  // 3 (p - 1), one rounding
   return r * __builtin_amdgcn_cosf(v);
 }
 // The two 16-bit angles of one word, in revolutions: high half -> t_l, low half -> t_m.

@@ -78,7 +78,8 @@ def t3_f32(u, v):
     """Student-t(3) by Bailey's trigonometric polar form: sqrt(3 (U^(-2/3) - 1)) cos(2 pi V)
     (csrc/philox.h:t3_f32; fp32 like the device's v_log/v_exp/v_sqrt/v_cos); v in revolutions."""
     p = np.exp2(np.float32(-2.0 / 3.0) * np.log2(u)).astype(np.float32)
-    r = np.sqrt(np.float32(3.0) * (p - np.float32(1.0))).astype(np.float32)
+    # fmaf(3, p, -3): 3 p - 3 is exact in fp64 (p >= 1 has 24 bits), then one rounding to fp32
+    r = np.sqrt((3.0 * p.astype(np.float64) - 3.0).astype(np.float32)).astype(np.float32)
     return (r * np.cos(v.astype(np.float64) * (2.0 * np.pi))).astype(np.float32)
 
 

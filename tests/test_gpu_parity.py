@@ -446,6 +446,26 @@ def test_device_fast_exp_accuracy(L):
     assert np.mean(out == ref) > 0.6
 
 
+def test_device_fast_log_accuracy(L):
+    """log_fast (csrc/fastmath.h), the Philox-mode logs of the z/tau draw (bi:200-225: log lambda,
+    log mu, the dropout time's uniform / truncated-exponential argument) and eta's normal:
+    <= 1 ulp from the correctly rounded log (tools/gen_log_table.py; 2 ulp allowed against numpy)
+    over the normal range, across every table bin and the binade edges, and exact at 1."""
+    rng = np.random.default_rng(4)
+    x = np.concatenate([np.exp(rng.uniform(-705, 705, 200_000)), rng.uniform(0.5, 2.0, 100_000),
+                        1.0 + rng.uniform(-2e-3, 2e-3, 50_000), rng.random(50_000) + 2.0 ** -53,
+                        np.array([1.0, 2.0, 0.5, 4.0, 1 - 2.0 ** -53, 1 + 2.0 ** -52, 2.0 ** -53, 2.0 ** -1022,
+                                  np.finfo(np.float64).max, 0.6865234375, 1.373046875])])
+    out = np.zeros_like(x)
+    assert L.clv_debug_log(_dp(x), x.size, _dp(out)) == 0
+    ref = np.log(x)
+    ulp = np.abs(out - ref) / np.spacing(np.abs(ref))
+    nz = ref != 0
+    assert ulp[nz].max() <= 2.0, (ulp[nz].max(), x[nz][np.argmax(ulp[nz])])
+    assert np.all(out[~nz] == 0.0)
+    assert np.mean(out == ref) > 0.6
+
+
 def _run_mode(p, persistent, sweeps, chunks, **kw):
     """Run `sweeps` sweeps in clv_run calls of `chunks` sizes with the persistent kernel on/off."""
     from mcmc_clv_model_amd.sampler import HipSampler

@@ -308,3 +308,52 @@ def test_multi_device_plan():
         multi_plan(4, 2, "summary+pct", "chains")
     with pytest.raises(ValueError, match="shard must be"):
         multi_plan(4, 2, "full", "rows")
+
+
+def test_fast_log_table_and_method():
+    """log_fast's table (tools/gen_log_table.py -> csrc/fastmath.h LOG_TAB) as compiled, and the
+    method with exact fma (fractions) against 60-digit logs: <= 1 ulp on a sample across the range."""
+    import math
+    import re
+    import struct
+    import sys
+    from decimal import Decimal, getcontext
+    from fractions import Fraction
+    ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import gen_log_table as g
+    src = open(os.path.join(ROOT, "mcmc_clv_model_amd", "csrc", "fastmath.h")).read()
+    body = src[src.index("LOG_TAB[2 * LOG_TAB_N] = {"):]
+    body = body[body.index("{") + 1:body.index("};")]
+    vals = [float.fromhex(v) for v in re.findall(r"-?0x[0-9a-fp.+-]+", body)]
+    tab = g.table()
+    assert vals == [v for pair in tab for v in pair]
+    hi, lo = g.ln2_split()
+    assert f"LOG_LN2_HI = {hi.hex()};" in src and f"LOG_LN2_LO = {lo.hex()};" in src
+    getcontext().prec = 60
+
+    def fma(a, b, c):
+        return float(Fraction(a) * Fraction(b) + Fraction(c))
+
+    def log_fast(x):
+        ix = struct.unpack("<Q", struct.pack("<d", x))[0]
+        h = ix >> 32
+        t = (h - g.OFF_HI) & 0xFFFFFFFF
+        k = (t - (1 << 32) if t >> 31 else t) >> 20
+        invc, logc = tab[(t >> 12) & 255]
+        z = struct.unpack("<d", struct.pack("<Q", (((h - (t & 0xFFF00000)) & 0xFFFFFFFF) << 32) | (ix & 0xFFFFFFFF)))[0]
+        r = fma(z, invc, -1.0)
+        assert abs(r) <= 2.0 ** -9
+        p = fma(r, -1.0 / 6.0, 1.0 / 5.0)
+        p = fma(p, r, -1.0 / 4.0)
+        p = fma(p, r, 1.0 / 3.0)
+        p = fma(p, r, -0.5)
+        return fma(float(k), hi, logc) + fma(float(k), lo, fma(r * r, p, r))
+
+    rng = np.random.default_rng(5)
+    xs = list(np.exp(rng.uniform(-700, 700, 400))) + list(rng.uniform(0.5, 2.0, 400)) + \
+        list(1.0 + rng.uniform(-2e-3, 2e-3, 200)) + [1.0, 2.0, 0.5, 1 - 2.0 ** -53, 1 + 2.0 ** -52, 2.0 ** -1022]
+    for x in xs:
+        x = float(x)
+        y, ref = log_fast(x), float(Decimal(x).ln())
+        assert (y == 0.0) if ref == 0.0 else abs(y - ref) <= math.ulp(ref), x
