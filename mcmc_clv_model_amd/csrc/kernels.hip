@@ -1234,18 +1234,37 @@ struct PreVariates {
   int lane;
 };
 
-__device__ __forceinline__ void mh_pre_variates(const SlotPhilox& ph, int S, const PreVariates& v) {
+// S is re-read as an opaque scalar at every call: held loop-invariant, the compiler hoisted the
+// per-step "k < S" lane masks out of the sweep loop and spilled them to VGPR lanes (2 v_readlane
+// + 1 v_cndmask per step); the padding select now runs only in a partial last chunk.
+__device__ __forceinline__ int opaque_uniform(int x) {
+  x = __builtin_amdgcn_readfirstlane(x);
+  asm volatile("" : "+s"(x));
+  return x;
+}
+
+__device__ __forceinline__ void mh_pre_variates(const SlotPhilox& ph, int S_, const PreVariates& v) {
   constexpr int MC = MH_CHUNK_STEPS;
+  const int S = opaque_uniform(S_);
 #pragma unroll
   for (int q = 0; q < PRE_STEPS / MC; ++q) {
     if (q * MC < S) {  // wave-uniform
       float tl[MC], tm[MC], lu[MC];
       mh_chunk_variates(ph, (uint32_t)q, tl, tm, lu);
+      if (q * MC + MC <= S) {  // full chunk
 #pragma unroll
-      for (int st = 0; st < MC; ++st) {
-        const int k = q * MC + st;
-        v.t[k * BLOCK + v.lane] = make_float2(tl[st], tm[st]);
-        v.u[k * BLOCK + v.lane] = k < S ? lu[st] : __builtin_inff();
+        for (int st = 0; st < MC; ++st) {
+          const int k = q * MC + st;
+          v.t[k * BLOCK + v.lane] = make_float2(tl[st], tm[st]);
+          v.u[k * BLOCK + v.lane] = lu[st];
+        }
+      } else {
+#pragma unroll
+        for (int st = 0; st < MC; ++st) {
+          const int k = q * MC + st;
+          v.t[k * BLOCK + v.lane] = make_float2(tl[st], tm[st]);
+          v.u[k * BLOCK + v.lane] = k < S ? lu[st] : __builtin_inff();
+        }
       }
     }
   }
@@ -1255,6 +1274,7 @@ template <int D, int K, bool CL>
 __device__ __forceinline__ void mh_run_pre(Cust<D, K, CL>& cu, const PreVariates& v, double s00, double s11, int S,
                                            const double* exp_tab) {
   constexpr int MC = MH_CHUNK_STEPS;
+  S = opaque_uniform(S);
 #pragma unroll
   for (int q = 0; q < PRE_STEPS / MC; ++q) {
     if (q * MC < S) {  // wave-uniform

@@ -71,10 +71,17 @@ CLV_HD u32x4 customer_block(uint32_t k0, uint32_t k1, uint32_t customer, uint32_
 // on (customer, key), so one sweep's blocks cost 18 instead of 20 multiplies.  Bit-identical to
 // customer_block() (checked by the device KAT test through clv_debug_variates).
 struct SlotPhilox {
-  uint32_t k0, k1, sweep;
+  uint32_t k0, k1, sk0;  // sk0 = sweep ^ k0, made wave-uniform (scalar registers) below
   uint32_t r1z, r1w;     // round-1 outputs that do not depend on the slot
   uint64_t p1r2;         // round-2 product M1 * r1z
-  CLV_HD SlotPhilox(uint32_t k0_, uint32_t k1_, uint32_t customer, uint32_t sweep_) : k0(k0_), k1(k1_), sweep(sweep_) {
+  CLV_HD SlotPhilox(uint32_t k0_, uint32_t k1_, uint32_t customer, uint32_t sweep_) : k0(k0_), k1(k1_) {
+    sk0 = sweep_ ^ k0_;
+#if defined(__HIP_DEVICE_COMPILE__)
+    // the sweep and key are uniform, but the compiler may hold them in vector registers (loop-carried
+    // sweep counters): without this, round 2's uniform M0 product ran per lane (2 v_mad_u64_u32 +
+    // 2 v_xor per block)
+    sk0 = __builtin_amdgcn_readfirstlane(sk0);
+#endif
     const uint64_t p0 = (uint64_t)0xD2511F53u * customer;
     r1z = (uint32_t)(p0 >> 32) ^ STREAM_CUSTOMER ^ k1_;
     r1w = (uint32_t)p0;
@@ -88,7 +95,7 @@ struct SlotPhilox {
 #endif
     // round 1 (key k): words x, y are uniform (plain xor: scalar unit)
     const uint64_t p1 = (uint64_t)0xCD9E8D57u * slot;
-    u32x4 c{(uint32_t)(p1 >> 32) ^ sweep ^ k0, (uint32_t)p1, r1z, r1w};
+    u32x4 c{(uint32_t)(p1 >> 32) ^ sk0, (uint32_t)p1, r1z, r1w};
     uint32_t a0 = k0 + 0x9E3779B9u, a1 = k1 + 0xBB67AE85u;
     // round 2: M0 * x is uniform, M1 * z (= p1r2) is slot-independent and hoisted; the uniform
     // parts of each xor are combined first, so each lane pays one v_xor
