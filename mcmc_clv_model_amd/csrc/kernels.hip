@@ -130,8 +130,9 @@ __device__ __forceinline__ void swap_rows(double& a, double& b) {
 template <int R>
 __device__ __forceinline__ double add_row_ror(double x) {
   const uint64_t u = dbits(x);
-  const uint32_t lo = __builtin_amdgcn_update_dpp(0u, (uint32_t)u, 0x120 + R, 0xf, 0xf, false);
-  const uint32_t hi = __builtin_amdgcn_update_dpp(0u, (uint32_t)(u >> 32), 0x120 + R, 0xf, 0xf, false);
+  // row_ror reads a valid lane everywhere: no "old" operand to initialise (v_mov_b32 0 per dword)
+  const uint32_t lo = __builtin_amdgcn_mov_dpp((uint32_t)u, 0x120 + R, 0xf, 0xf, true);
+  const uint32_t hi = __builtin_amdgcn_mov_dpp((uint32_t)(u >> 32), 0x120 + R, 0xf, 0xf, true);
   return x + bitsd(((uint64_t)hi << 32) | lo);
 }
 
@@ -286,7 +287,9 @@ struct StatGen {
     } else {
       v = lik;
     }
-    return on ? 0.0 + v : 0.0;
+    // no select on `on`: an inactive lane's StatGen is value-initialised (all inputs 0), so its
+    // products are exact zeros already
+    return v;
   }
 };
 
@@ -1155,8 +1158,8 @@ __device__ __forceinline__ double clip70_fma(double a, double b, double c) {
 
 // One Philox-mode MH step (bi:316-335) with lp(proposal) = -inf for pm > 5 (Q3): accept iff
 // pm <= 5 and exp(plp - cur) > u  <=>  plp > cur + log(u)  (cur = -inf accepts any finite one;
-// cur + log u is formed off the dependent chain, alongside the proposal; a padded step's
-// log u = +inf gives +inf or NaN there, never accepted).
+// cur + log u = fma(log2 u, ln 2, cur) is formed off the dependent chain, alongside the proposal;
+// a padded step's log2 u = +inf gives +inf or NaN there, never accepted).
 // The log mu proposal needs only the lower bound: a proposal above 5 is rejected by the Q3 cap
 // whatever its value (and its log posterior, even NaN, is then never looked at), and an accepted
 // one is <= 5 < 70, so max(., -70) accepts exactly what clip(., -70, 70) does.
@@ -1168,9 +1171,9 @@ __device__ __forceinline__ double prop_lm(double a, double b, double c) {
 }
 
 template <int D, int K, bool CL>
-__device__ __forceinline__ void mh_step(Cust<D, K, CL>& u, double s00, double s11, float t_l, float t_m, float l_u,
+__device__ __forceinline__ void mh_step(Cust<D, K, CL>& u, double s00, double s11, float t_l, float t_m, float l2u,
                                         const double* exp_tab) {
-  const double thr = u.cur + (double)l_u;
+  const double thr = __builtin_fma((double)l2u, 0x1.62e42fefa39efp-1, u.cur);  // cur + ln2 log2 u
   const double pl = clip70_fma(s00, (double)t_l, u.ll);
   const double pm = prop_lm(s11, (double)t_m, u.lm);
   const double plp = log_post_fast(u.fc, pl, pm, exp_tab);

@@ -131,8 +131,8 @@ CLV_HD void chain_key(uint64_t seed, int64_t chain, uint32_t* k0, uint32_t* k1) 
 __device__ __forceinline__ float uf32(uint32_t w) {
   return __builtin_fmaf((float)w, 0x1.0p-32f, 0x1.0p-33f);
 }
-__device__ __forceinline__ float ln_f32(float u) {  // natural log via v_log_f32 (log2)
-  return __builtin_amdgcn_logf(u) * 0.69314718055994530942f;
+__device__ __forceinline__ float log2_f32(float u) {  // v_log_f32 (the MH step scales by ln 2 in fp64)
+  return __builtin_amdgcn_logf(u);
 }
 // Student-t(3) by Bailey's trigonometric form of the polar method (Bailey 1994, Math. Comp.
 // 62:779-781): R^2 = nu (U^(-2/nu) - 1) is the squared radius of a spherical bivariate t_nu, so
@@ -145,24 +145,26 @@ __device__ __forceinline__ float t3_f32(float u, float v) {
   return r * __builtin_amdgcn_cosf(v);
 }
 // The two 16-bit angles of one word, in revolutions: high half -> t_l, low half -> t_m.
-__device__ __forceinline__ float angle_hi(uint32_t w) { return (float)(w & 0xffff0000u) * 0x1.0p-32f; }
-__device__ __forceinline__ float angle_lo(uint32_t w) { return (float)(w << 16) * 0x1.0p-32f; }
+// (float) of a 16-bit half is one v_cvt_f32_u32 with an SDWA word select; both are exact, so the
+// values equal (w & 0xffff0000) * 2^-32 and (w << 16) * 2^-32.
+__device__ __forceinline__ float angle_hi(uint32_t w) { return (float)(w >> 16) * 0x1.0p-16f; }
+__device__ __forceinline__ float angle_lo(uint32_t w) { return (float)(w & 0xffffu) * 0x1.0p-16f; }
 
 // Words of the MH steps: step j uses the four words of Philox block SLOT_MH0 + j:
 // x = radius uniform of t_l, y = radius uniform of t_m, z = the two angles (16 bits each),
 // w = accept uniform.  Chunk q = steps 4q .. 4q+3.
 constexpr int MH_CHUNK_STEPS = 4;
 
-// One chunk's variates: t_l, t_m and log(U_accept) of 4 consecutive MH steps.
+// One chunk's variates: t_l, t_m and log2(U_accept) of 4 consecutive MH steps.
 template <class PH>
 __device__ __forceinline__ void mh_chunk_variates(const PH& ph, uint32_t q, float (&t_l)[4], float (&t_m)[4],
-                                                  float (&log_u)[4]) {
+                                                  float (&log2_u)[4]) {
 #pragma unroll
   for (int i = 0; i < MH_CHUNK_STEPS; ++i) {
     const u32x4 r = ph(SLOT_MH0 + (uint32_t)MH_CHUNK_STEPS * q + (uint32_t)i);
     t_l[i] = t3_f32(uf32(r.x), angle_hi(r.z));
     t_m[i] = t3_f32(uf32(r.y), angle_lo(r.z));
-    log_u[i] = ln_f32(uf32(r.w));
+    log2_u[i] = log2_f32(uf32(r.w));
   }
 }
 
