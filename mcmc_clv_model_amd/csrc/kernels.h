@@ -23,6 +23,7 @@ enum : int {
   H_P00 = 36, H_P01 = 37, H_P11 = 38,  // inv(Sigma)[0:2,0:2] (bi:283, tri:402 quirk Q4)
   H_S00 = 39, H_S11 = 40,              // proposal scales Sigma[0,0], Sigma[1,1] (quirk Q2)
   H_S22 = 41, H_POSTVAR = 42, H_SQRT_POSTVAR = 43, H_OMEGA2 = 44,  // draw_eta (tri:321-333)
+  H_INV_OMEGA2 = 45, H_INV_S22 = 46,   // 1 / omega2, 1 / Sigma[2,2] (Philox-mode draw_eta)
 };
 
 struct Ctrl {

@@ -427,6 +427,8 @@ __device__ void finalize_hyper(const double* beta_flat, const double (&Sig)[D][D
     hput<TO_LDS>(H, H_POSTVAR, post_var);
     hput<TO_LDS>(H, H_SQRT_POSTVAR, sqrt(post_var));
     hput<TO_LDS>(H, H_OMEGA2, omega2);
+    hput<TO_LDS>(H, H_INV_OMEGA2, 1.0 / omega2);
+    hput<TO_LDS>(H, H_INV_S22, 1.0 / Sig[2][2]);
   }
   hput<TO_LDS>(H, H_S00, Sig[0][0]);
   hput<TO_LDS>(H, H_S11, Sig[1][1]);
@@ -1306,7 +1308,7 @@ struct CustOut {
 // sweep s+1 in the level-2 hand-off window (with the MH variates), off the sweep's serial path.
 __device__ __forceinline__ double eta_normal(uint32_t k0, uint32_t k1, uint32_t gi, int64_t s, const double* tab) {
   const u32x4 r = customer_block(k0, k1, gi, (uint32_t)s, SLOT_ETA);
-  return sqrt(-2.0 * log_fast(u53_open0(r.x, r.y), tab)) * cospi(2.0 * u53(r.z, r.w));
+  return sqrt(-2.0 * log_fast(u53_open0(r.x, r.y), tab)) * cos2pi_u53(r.z, r.w, tab);  // tab: FAST_TAB_N3
 }
 
 template <int D, int K, bool REPLAY, bool CL>
@@ -1331,7 +1333,9 @@ __device__ __forceinline__ CustOut<D> cust_finish(Cust<D, K, CL>& u, const Sweep
 #pragma unroll
     for (int k = 0; k < K; ++k) m2 += u.x(k) * H[H_BETA + k * D + 2];
     const double post_var = H[H_POSTVAR];
-    const double post_mean = post_var * (a.log_s[i] / H[H_OMEGA2] + m2 / H[H_S22]);
+    // Philox mode: the reciprocals come with the hyper state (no per-customer fp64 division)
+    const double post_mean = REPLAY ? post_var * (a.log_s[i] / H[H_OMEGA2] + m2 / H[H_S22])
+                                    : post_var * __builtin_fma(a.log_s[i], H[H_INV_OMEGA2], m2 * H[H_INV_S22]);
     double zeta;
     if constexpr (REPLAY) {
       zeta = tape[(int64_t)(2 + 3 * g.S) * g.n + i];
@@ -1436,15 +1440,19 @@ __device__ __forceinline__ void sweep_body(const SweepArgs& a) {
   constexpr int NS = NXY + NYY + 1;
   __shared__ double red[BLOCK / 64][NS];
   __shared__ double tot[NS];
-  __shared__ __attribute__((aligned(16))) double exp_tab[FAST_TAB_N];
-  // the exp/log table's global loads are issued first; they are stored to LDS (and the barrier
-  // taken) after the customer's own loads are in flight
-  static_assert(BLOCK == EXP_TAB_N && BLOCK == LOG_TAB_N, "one table entry per thread");
-  double tab_v = 0.0, tab_l0 = 0.0, tab_l1 = 0.0;
+  __shared__ __attribute__((aligned(16))) double exp_tab[D == 3 ? FAST_TAB_N3 : FAST_TAB_N];
+  // the exp/log(/cos) table's global loads are issued first; they are stored to LDS (and the
+  // barrier taken) after the customer's own loads are in flight
+  static_assert(BLOCK == EXP_TAB_N && BLOCK == LOG_TAB_N && BLOCK == COS_TAB_N, "one table entry per thread");
+  double tab_v = 0.0, tab_l0 = 0.0, tab_l1 = 0.0, tab_c0 = 0.0, tab_c1 = 0.0;
   if (!REPLAY) {
     tab_v = EXP2_TAB[threadIdx.x];
     tab_l0 = LOG_TAB[2 * threadIdx.x];
     tab_l1 = LOG_TAB[2 * threadIdx.x + 1];
+    if constexpr (D == 3) {
+      tab_c0 = COS_TAB[2 * threadIdx.x];
+      tab_c1 = COS_TAB[2 * threadIdx.x + 1];
+    }
   }
 
   const Geometry& g = a.g;
@@ -1506,6 +1514,10 @@ __device__ __forceinline__ void sweep_body(const SweepArgs& a) {
     exp_tab[threadIdx.x] = tab_v;
     exp_tab[EXP_TAB_N + 2 * threadIdx.x] = tab_l0;
     exp_tab[EXP_TAB_N + 2 * threadIdx.x + 1] = tab_l1;
+    if constexpr (D == 3) {
+      exp_tab[FAST_TAB_N + 2 * threadIdx.x] = tab_c0;
+      exp_tab[FAST_TAB_N + 2 * threadIdx.x + 1] = tab_c1;
+    }
   }
   __syncthreads();
   if (threadIdx.x == 0 && !a.init) CLV_WG_STAMP(a.stamps, (int64_t)c * g.nb_local + b, 8);
@@ -2068,7 +2080,7 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
   constexpr int NTRIL = D * (D - 1) / 2;
   __shared__ double red[BLOCK / 64][NS];
   __shared__ double tot[NS];
-  __shared__ __attribute__((aligned(16))) double exp_tab[FAST_TAB_N];
+  __shared__ __attribute__((aligned(16))) double exp_tab[D == 3 ? FAST_TAB_N3 : FAST_TAB_N];
   __shared__ double Hs[HS];
   __shared__ uint32_t s_abort;
   // customer workgroups: the drawn-ahead MH variates; the level-2 workgroup (P2P): its unit partials
@@ -2105,7 +2117,7 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
     cu.i = cu.active ? i : (g.n > 0 ? g.n - 1 : 0);
   }
   cust_load(cu, a, c);  // once per launch: CBS row, covariates, state stay in registers
-  fast_tab_fill(exp_tab, tid, BLOCK);
+  fast_tab_fill(exp_tab, tid, BLOCK, D == 3);
   if (tid < HS) Hs[tid] = a.hyper[(int64_t)c * HS + tid];  // sweep s_first: from before this launch
   __syncthreads();
   if (cu.active) cust_ztau<D, K, false>(cu, a, s_first, k0, k1, nullptr, exp_tab);
@@ -2227,8 +2239,8 @@ __global__ void debug_philox_kernel(uint32_t k0, uint32_t k1, const uint32_t* ct
 
 __global__ void debug_variates_kernel(uint64_t seed, int chain, uint32_t sweep, int64_t n, int S, float* tl,
                                       float* tm, float* ua, double* uz, double* ut, double* ea, double* ez) {
-  __shared__ __attribute__((aligned(16))) double tab[FAST_TAB_N];
-  fast_tab_fill(tab, threadIdx.x, blockDim.x);
+  __shared__ __attribute__((aligned(16))) double tab[FAST_TAB_N3];
+  fast_tab_fill(tab, threadIdx.x, blockDim.x, true);
   __syncthreads();
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;

@@ -1,4 +1,5 @@
-"""Regenerates the log_fast constants of mcmc_clv_model_amd/csrc/fastmath.h (LOG_TAB, ln2 split).
+"""Regenerates the log_fast and cos2pi_u53 tables of mcmc_clv_model_amd/csrc/fastmath.h (COS_TAB,
+LOG_TAB, the ln2 split).
 
 log_fast(x), x > 0 normal:  x = 2^k z with z in [OFF, 2 OFF), OFF = 0x3fe5f800_00000000 (~0.6865),
 read off the high word h of x:  t = h - 0x3fe5f800,  k = t >> 20 (arithmetic),  bin i = (t >> 12) & 255,
@@ -45,7 +46,39 @@ def ln2_split():
     return hi, float(ln2 - Decimal(hi))
 
 
+def cos_table():
+    """(cos, sin) of 2 pi j / 1024, j = 0..255 (the first quadrant in 256 steps), 60-digit."""
+    from decimal import Decimal as Dd
+    getcontext().prec = 60
+    pi = Dd("3.14159265358979323846264338327950288419716939937510582097494459")
+    out = []
+    for j in range(256):
+        a = 2 * pi * j / 1024
+        # Taylor series at 60 digits (|a| < pi / 2)
+        c, s, term, k = Dd(0), Dd(0), Dd(1), 0
+        while True:
+            if k % 4 == 0:
+                c += term
+            elif k % 4 == 1:
+                s += term
+            elif k % 4 == 2:
+                c -= term
+            else:
+                s -= term
+            k += 1
+            term = term * a / k
+            if abs(term) < Dd(10) ** -58:
+                break
+        out.append((float(c), float(s)))
+    return out
+
+
 def main():
+    print("__device__ constexpr double COS_TAB[2 * COS_TAB_N] = {  // (cos, sin) of 2 pi j / 1024")
+    rows = [f"{a.hex()}, {b.hex()}," for a, b in cos_table()]
+    for j in range(0, 256, 2):
+        print("    " + " ".join(rows[j:j + 2]))
+    print("};")
     hi, lo = ln2_split()
     print(f"constexpr uint32_t LOG_OFF_HI = 0x{OFF_HI:08x}u;")
     print(f"constexpr double LOG_LN2_HI = {hi.hex()};")
