@@ -192,7 +192,8 @@ int clv_read_draws(clv_sampler* s, double* level1, double* level2, double* logli
 int clv_read_summary(clv_sampler* s, double* sums, int64_t* n_stored);
 
 /* Current state: lambda, mu [chain][n]; hyper [chain][beta K*D, Sigma D*D]. Setting the state
- * is exact resume (the Philox counter is the sweep index). */
+ * is exact resume (the Philox counter is the sweep index); lambdas and mus must be positive,
+ * normal and finite (CLV_EINVAL otherwise: the sweep takes their logs, bi:286-287). */
 int clv_get_state(clv_sampler* s, double* lambdas, double* mus, double* hyper);
 int clv_set_state(clv_sampler* s, const double* lambdas, const double* mus, const double* hyper,
                   int64_t sweeps_done);
@@ -232,12 +233,13 @@ int clv_debug_exp(const double* x, int64_t n, double* out);
  * draw's logs (bi:200-225) and the eta normal's radius. */
 int clv_debug_log(const double* x, int64_t n, double* out);
 /* One Philox-mode MH step exactly as the sweep kernels run it (bi:291-335: log posterior with the
- * Q3 cap, fma + clip proposal, accept iff pm <= 5 and plp > cur + log U), on n independent lanes.
- * Per lane: x, z, T_cal, tau, mean [n][2] (X @ beta), cur_pt [n][2] (log lambda, log mu), t3 [n][2]
- * (fp32 t3 noise), log_u (fp32, +inf = a padded step); shared prec3 = inv(Sigma)[0:2,0:2] as
- * (p00, p01, p11) and scale2 = (Sigma00, Sigma11) (Q2).  out [n][7] = current log posterior (up
- * to a per-customer constant), the proposal's (before the Q3 cap), the proposal (pl, pm), the new
- * log lambda, log mu and log posterior. */
+ * Q3 cap, fma + clip proposal, accept iff pm <= 5 and plp > cur + ln2 log2 U), on n independent
+ * lanes.  Per lane: x, z, T_cal, tau, mean [n][2] (X @ beta), cur_pt [n][2] (log lambda, log mu),
+ * t3 [n][2] (fp32 t3 noise), log_u = log2 U (fp32, as the sweeps draw it; +inf = a padded step);
+ * shared prec3 = inv(Sigma)[0:2,0:2] as (p00, p01, p11) and scale2 = (Sigma00, Sigma11) (Q2).
+ * out [n][7] = current log posterior (up to a per-customer constant), the proposal's (before the
+ * Q3 cap), the proposal (pl, pm; pm clipped below only: one above 5 is rejected whatever it is),
+ * the new log lambda, log mu and log posterior. */
 int clv_debug_mh_step(int64_t n, const int32_t* x, const uint8_t* z, const double* T_cal, const double* tau,
                       const double* mean, const double* prec3, const double* cur_pt, const float* t3,
                       const double* scale2, const float* log_u, double* out);

@@ -1045,8 +1045,15 @@ int clv_get_state(clv_sampler* s, double* lambdas, double* mus, double* hyper) {
 
 int clv_set_state(clv_sampler* s, const double* lambdas, const double* mus, const double* hyper, int64_t sweeps_done) {
   if (!s || sweeps_done < 0) return fail(CLV_EINVAL, "bad arguments");
-  CLV_HIP(hipSetDevice(s->device));
   const Geometry& g = s->g;
+  // the sampler takes logs of the state (bi:286-287; Philox mode: log_fast, defined for positive
+  // normal doubles): reject what exp() of a log-scale state can never be
+  for (const double* v : {lambdas, mus})
+    if (v)
+      for (int64_t i = 0; i < (int64_t)g.n_chains * g.n; ++i)
+        if (!(v[i] >= 2.2250738585072014e-308 && v[i] <= 1.7976931348623157e308))
+          return fail(CLV_EINVAL, "lambdas and mus must be positive, normal and finite");
+  CLV_HIP(hipSetDevice(s->device));
   if (lambdas && g.n) CLV_HIP(hipMemcpy(s->d_lam, lambdas, sizeof(double) * g.n_chains * g.n, hipMemcpyHostToDevice));
   if (mus && g.n) CLV_HIP(hipMemcpy(s->d_mu, mus, sizeof(double) * g.n_chains * g.n, hipMemcpyHostToDevice));
   if (hyper) {

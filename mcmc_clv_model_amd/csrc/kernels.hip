@@ -337,11 +337,23 @@ __device__ __forceinline__ int64_t uniform_i64(int64_t v) {
   return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
+// s is wave-uniform at every call site and sweep counts are 32-bit (clv_config): the offset is
+// made explicitly uniform so the modulo / division run on the scalar unit (the persistent kernel
+// holds its loop counter in vector registers, where they were ~60 VALU of 64-bit division emulation
+// per sweep and lane).
+__device__ __forceinline__ int64_t uniform64(int64_t x) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)x >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ uint32_t stored_offset(int64_t s, const Geometry& g) {
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(s - 1 - g.burnin));
+}
 __device__ __forceinline__ bool is_stored(int64_t s, const Geometry& g) {
-  return s > g.burnin && s <= (int64_t)g.burnin + g.mcmc && ((s - 1 - g.burnin) % g.thin) == 0;
+  return s > g.burnin && s <= (int64_t)g.burnin + g.mcmc && stored_offset(s, g) % (uint32_t)g.thin == 0u;
 }
 __device__ __forceinline__ int64_t draw_index(int64_t s, const Geometry& g) {
-  return (s - 1 - g.burnin) / g.thin;
+  return (int64_t)(stored_offset(s, g) / (uint32_t)g.thin);  // (only called for stored sweeps: s > burnin)
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2133,7 +2145,7 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
     // Philox products of the customer counter word are the same every sweep; hoisted out of the
     // loop they were kept live (and spilled, tri K=3) — recomputed per sweep instead (a few VALU)
     if constexpr (CLV_OPAQUE_GI(D)) asm volatile("" : "+v"(cu.gi));
-    const int64_t s = s_first + it;
+    const int64_t s = uniform64(s_first + it);  // scalar registers: the sweep's address and index arithmetic on the scalar unit
     const bool stored = is_stored(s, g);
     const bool stp = tid == 0 && it == it_stamp;
     (void)stp;

@@ -203,6 +203,12 @@ def test_resume_from_state_is_exact(L):
             got = s.get_state()
         for x, y in zip(ref, got):
             assert np.array_equal(bits(x), bits(y))
+        with HipSampler(p, **kw) as s:  # states exp() of a log-scale state can never take
+            lam, mu = st[0].copy(), st[1].copy()
+            for bad in (0.0, -1.0, np.inf, np.nan, 1e-310):
+                lam[0, 3] = bad
+                with pytest.raises(ValueError, match="positive, normal and finite"):
+                    s.set_state(lam, mu, st[2], st[3], sweeps_done=4)
 
 
 def test_storage_indexing_and_summary_sink(L):
@@ -518,7 +524,7 @@ def test_persistent_kernel_bitwise_equals_launch_per_sweep(L, D, covs, n, sink, 
 
 
 def _mh_step_device(L, f, t3, log_u, cur_pt=None):
-    """clv_debug_mh_step over formulas.npz's log-posterior inputs (G1, bi:291-310)."""
+    """clv_debug_mh_step over formulas.npz's log-posterior inputs (G1, bi:291-310); log_u is log2 U."""
     n = f["lp_ll"].size
     S = f["lp_S"]
     P = np.linalg.inv(S)
@@ -575,7 +581,10 @@ def test_device_mh_step_matches_reference_log_posterior(L):
     lu[near] = (np.minimum(d_ref[near], 0.0) + rng.choice([-1, 1], near.sum()) * 10.0 ** rng.uniform(-6, -1, near.sum())
                 ).astype(np.float32)
     lu = np.minimum(lu, np.float32(-1e-30))  # log U < 0 (U < 1)
-    out = _mh_step_device(L, f, t3, lu)
+    # the step takes log2 U (fp32) and forms cur + ln2 log2 U in fp64: the reference sees that log U
+    lu2 = (lu.astype(np.float64) / np.log(2.0)).astype(np.float32)
+    lu = lu2.astype(np.float64) * np.log(2.0)
+    out = _mh_step_device(L, f, t3, lu2)
     cur, plp = out[:, 0], out[:, 1]
     # Q3 on the current point
     assert np.all(np.isneginf(cur[f["lp_lm"] > 5.0])) and np.all(np.isfinite(cur[f["lp_lm"] <= 5.0]))
