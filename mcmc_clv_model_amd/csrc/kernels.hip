@@ -681,42 +681,52 @@ __device__ void level2_draw_fast(const double* tot, const double* iwn, const dou
       } else {
         bartlett_inverse<D>(iwn, chi2, Ai);
       }
+      // One lane issues in order, so every sum below runs its terms in the reference order per
+      // element but with the independent elements' chains interleaved (term-major loops): the
+      // dependent fp64 latency is paid once per term, not once per term and element.
       double R[NXY], Bh[NXY];
 #pragma unroll
       for (int q = 0; q < NXY; ++q) R[q] = tot[q] + A0B0[q];
 #pragma unroll
-      for (int q = 0; q < NXY; ++q) {  // B_hat[k][d] = sum_j V[k][j] R[j][d]
-        const int k = q / D, d = q % D;
-        double sv = 0.0;
+      for (int q = 0; q < NXY; ++q) Bh[q] = 0.0;
 #pragma unroll
-        for (int j = 0; j < K; ++j) sv += V[k * K + j] * R[j * D + d];
-        Bh[q] = sv;
-      }
-      double Sn[D][D];
+      for (int j = 0; j < K; ++j)  // B_hat[k][d] = sum_j V[k][j] R[j][d]
+#pragma unroll
+        for (int q = 0; q < NXY; ++q) Bh[q] += V[(q / D) * K + j] * R[j * D + q % D];
+      double Sn[D][D], rb[D][D];
+#pragma unroll
+      for (int p = 0; p < D; ++p)
+#pragma unroll
+        for (int q = p; q < D; ++q) rb[p][q] = 0.0;
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+#pragma unroll
+        for (int p = 0; p < D; ++p)
+#pragma unroll
+          for (int q = p; q < D; ++q) rb[p][q] += R[k * D + p] * Bh[k * D + q];
       int n = NXY;
 #pragma unroll
       for (int p = 0; p < D; ++p)
 #pragma unroll
         for (int q = p; q < D; ++q) {
-          double rb = 0.0;
-#pragma unroll
-          for (int k = 0; k < K; ++k) rb += R[k * D + p] * Bh[k * D + q];
-          Sn[p][q] = (S0B[p * D + q] + tot[n++]) - rb;
+          Sn[p][q] = (S0B[p * D + q] + tot[n++]) - rb[p][q];
           Sn[q][p] = Sn[p][q];
         }
       double Sig[D][D], M[D][D];
       iw_core_fast<D>(Sn, Ai, Sig, M);
       asm volatile("" ::: "memory");  // chol(V) and the noise are read here, not hoisted above (registers)
+      double sv[NXY];
 #pragma unroll
-      for (int q = 0; q < NXY; ++q) {  // beta = B_hat + kron(chol Sigma, chol V) z, row-major ravel (Q1)
-        const int p = q / K, bq = q % K;
-        double sv = 0.0;
+      for (int q = 0; q < NXY; ++q) sv[q] = 0.0;
 #pragma unroll
-        for (int cc = 0; cc <= p; ++cc)
+      for (int cc = 0; cc < D; ++cc)  // beta = B_hat + kron(chol Sigma, chol V) z, row-major ravel (Q1);
+#pragma unroll                      // per element the terms (cc <= p, e <= bq) in cc-major order
+        for (int e = 0; e < K; ++e)
 #pragma unroll
-          for (int e = 0; e <= bq; ++e) sv += M[p][cc] * cholV[bq * K + e] * noise[cc * K + e];
-        sc->beta[q] = Bh[q] + sv;
-      }
+          for (int q = 0; q < NXY; ++q)
+            if (cc <= q / K && e <= q % K) sv[q] += M[q / K][cc] * cholV[(q % K) * K + e] * noise[cc * K + e];
+#pragma unroll
+      for (int q = 0; q < NXY; ++q) sc->beta[q] = Bh[q] + sv[q];
 #pragma unroll
       for (int p = 0; p < D; ++p)
 #pragma unroll
@@ -778,8 +788,13 @@ __device__ void level2_draw_fast(const double* tot, const double* iwn, const dou
     if (t < NXY) {
       const int p = t / K, bq = t % K;
       double sv = 0.0;
-      for (int cc = 0; cc <= p; ++cc)
-        for (int e = 0; e <= bq; ++e) sv += sc->Ls[p * D + cc] * cholV[bq * K + e] * noise[cc * K + e];
+#pragma unroll
+      for (int cc = 0; cc < D; ++cc)  // fully unrolled: the LDS reads go out together; the terms
+#pragma unroll                      // (cc <= p, e <= bq) are added in the same order as before
+        for (int e = 0; e < K; ++e) {
+          const double term = sc->Ls[p * D + cc] * cholV[bq * K + e] * noise[cc * K + e];
+          sv = (cc <= p && e <= bq) ? sv + term : sv;
+        }
       sc->beta[t] = sc->Bh[t] + sv;
     }
     wave_sync();
@@ -891,6 +906,9 @@ __device__ void hyper_finish(const HyperArgs& a, int c, int64_t s, int mode, dou
   if (tid == 0) CLV_STAMP(a.stamps, s, 6, false);
   L2Scratch* sc = l2;
   level2_draw<D, K>(tot, var_iw, var_chi, var_noise, REPLAY, sc);
+#ifdef CLV_STAMP_L2SPLIT  // diagnostic: slot 5 = the level-2 draw's end (before finalize_hyper)
+  if (tid == 0) CLV_STAMP(a.stamps, s, 5, false);
+#endif
   const bool store_l2 = hs >= 1 && is_stored(hs, g);
   double* o = store_l2 ? a.level2 + ((int64_t)c * g.n_draws + draw_index(hs, g)) * g.l2w : nullptr;
   if (tid < K * D && store_l2) o[(tid % D) * K + tid / D] = sc->beta[tid];  // beta.T.ravel() (bi:411)
@@ -1496,7 +1514,9 @@ __device__ __forceinline__ void sweep_body(const SweepArgs& a) {
   StatGen<D, K> st{};
   if (threadIdx.x == 0 && !a.init) {
     CLV_STAMP(a.stamps, s, 0, true);
+#ifndef CLV_STAMP_L2SPLIT
     CLV_STAMP(a.stamps, s, 5, false);
+#endif
     CLV_WG_STAMP(a.stamps, (int64_t)c * g.nb_local + b, 0);
     CLV_WG_STAMP(a.stamps, (int64_t)c * g.nb_local + b, 2);
     CLV_WG_STAMP(a.stamps, (int64_t)c * g.nb_local + b, 3);

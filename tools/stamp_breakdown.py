@@ -43,6 +43,9 @@ def main(workload="c2", sweeps=1500, chains=None):
     print(f"    tail: unit reduction                  {us(st[:, 6] - st[:, 2]):8.2f} us")
     print(f"    tail: level-2 algebra (one lane)      {us(st[:, 7] - st[:, 6]):8.2f} us")
     print(f"    tail: record + counters               {us(st[:, 3] - st[:, 7]):8.2f} us")
+    if os.environ.get("CLV_STAMP_L2SPLIT"):  # a build with -DCLV_STAMP_L2SPLIT: slot 5 = draw end
+        print(f"      algebra: level2_draw                {us(st[:, 5] - st[:, 6]):8.2f} us")
+        print(f"      algebra: finalize_hyper             {us(st[:, 7] - st[:, 5]):8.2f} us")
     # placement of the latest launch's workgroups: per CU (XCC, SE, CU) count and durations
     nb = -(-s.n // 256)
     wg = np.zeros(s.chains * (nb + 1) * 12, np.uint64)
