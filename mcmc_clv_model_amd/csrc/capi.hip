@@ -229,6 +229,8 @@ int64_t clv_replay_sweep_stride(const clv_sampler* s) {
   return n * (2 + 3 * (int64_t)s->g.S + (s->g.D == 3 ? 1 : 0)) + TAPE_HYPER;
 }
 
+}  // extern "C"
+
 namespace {
 // Persistent grid: which (chain, block) each dispatched workgroup runs.  The grid has more
 // workgroups (T = chains x (blocks + 1)) than CUs, and the dispatcher fills every CU once before
@@ -295,6 +297,8 @@ std::vector<int32_t> persist_wg_map(int C, int nb, int n_cu) {
   return map;
 }
 }  // namespace
+
+extern "C" {
 
 int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* prior, clv_sampler** out) {
   if (!cfg || !data || !prior || !out) return fail(CLV_EINVAL, "null argument");

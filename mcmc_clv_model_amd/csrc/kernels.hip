@@ -2105,11 +2105,9 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
 // kernel carries none of its registers or LDS).
 template <int D, int K, bool P2P>
 __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t s_first, int64_t n_sweeps) {
-  constexpr int NT = BLOCK;
   constexpr int NXY = K * D;
   constexpr int NYY = D * (D + 1) / 2;
   constexpr int NS = NXY + NYY + 1;
-  constexpr int NTRIL = D * (D - 1) / 2;
   __shared__ double red[BLOCK / 64][NS];
   __shared__ double tot[NS];
   __shared__ __attribute__((aligned(16))) double exp_tab[D == 3 ? FAST_TAB_N3 : FAST_TAB_N];
