@@ -156,8 +156,9 @@ int clv_launch_info(const clv_sampler* s, int64_t* out);
  * own mail holds all ranks' units, and sums them in the same global unit order as clv_hyper — so
  * results are bitwise those of clv_sweep/clv_hyper with an all-gather (and of world size 1).
  * Replaces, per sweep, the all-gather of bi:243-255's statistics.
- *   clv_p2p_info:    out[5] = (capable 0/1, connected 0/1, mail bytes, mail device pointer,
- *                    persistent 0/1); persistent = every workgroup of the persistent grid fits at
+ *   clv_p2p_info:    out[6] = (capable 0/1, connected 0/1, mail bytes, mail device pointer,
+ *                    persistent 0/1, mail memory: 0 uncached / 1 fine-grained / 2 device default /
+ *                    -1 none); persistent = every workgroup of the persistent grid fits at
  *                    once on this GPU.  Otherwise (any shard size) clv_run launches the sweep
  *                    kernel once per sweep and its fused level-2 tail exchanges the same way: the
  *                    chain's unit-last workgroups store this rank's unit partials into every rank's
@@ -177,6 +178,14 @@ int clv_launch_info(const clv_sampler* s, int64_t* out);
 int clv_p2p_info(const clv_sampler* s, int64_t* out);
 int clv_p2p_export(clv_sampler* s, void* handle);
 int clv_p2p_connect(clv_sampler* s, const void* handles, const uint64_t* ptrs);
+/* Drop the peer connection (closes opened IPC mappings, forgets the peers' mail pointers): a sharded
+ * clv_run then fails with CLV_ESTATE until clv_p2p_connect is called again.  Idempotent. */
+int clv_p2p_disconnect(clv_sampler* s);
+/* Bound of every wait in the persistent / fused-exchange kernels, in ms (default 2000 at world size
+ * 1, 10000 with peers; the CLV_WAIT_TIMEOUT_MS environment variable sets the default at create).
+ * A short bound makes a failed peer-exchange check cheap (distributed.ShardedSampler's verification
+ * runs under 500 ms). */
+int clv_set_wait_timeout(clv_sampler* s, double ms);
 /* Launch on another stream from now on (e.g. a stream under hipGraph capture by the caller,
  * who then replays the captured sweeps), and adjust the host's sweep count by n (+chunk per
  * replay; -chunk after a capture, which records launches without executing them). */
@@ -258,7 +267,9 @@ int clv_debug_wg_map(int32_t n_chains, int32_t nb, int32_t n_cu, int32_t* out);
  *   CLV_EXCHANGE_COPY: per sweep the sweep kernels, device-to-device copies of each shard's unit
  *                      partials into every shard's gathered buffer (stream-ordered by events), and
  *                      every shard's level-2 draw.
- * CLV_EXCHANGE_AUTO picks P2P where possible.  Results are bitwise those of the unsharded run.  A
+ * CLV_EXCHANGE_AUTO picks P2P where possible and no two shards share a device (their persistent
+ * kernels would have to run concurrently from different streams, which HIP does not promise); the
+ * group disconnects the shards it connected when destroyed.  Results are bitwise those of the unsharded run.  A
  * P2P call that times out on any shard is undone on the others and redone by copies (kept).
  * clv_group_run is synchronous; the bivariate initial draw (bi:393 of sweep 1) is its first
  * exchange.  The group does not own the shards (destroy the group first). */

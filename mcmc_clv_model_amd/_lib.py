@@ -99,6 +99,8 @@ def lib() -> ctypes.CDLL:
         "clv_p2p_info": (c_int32, [sp, POINTER(c_int64)]),
         "clv_p2p_export": (c_int32, [sp, c_void_p]),
         "clv_p2p_connect": (c_int32, [sp, c_void_p, POINTER(c_uint64)]),
+        "clv_p2p_disconnect": (c_int32, [sp]),
+        "clv_set_wait_timeout": (c_int32, [sp, c_double]),
         "clv_set_stream": (c_int32, [sp, c_uint64]),
         "clv_note_sweeps": (c_int32, [sp, c_int64]),
         "clv_read_draws": (c_int32, [sp, dp, dp, dp]),

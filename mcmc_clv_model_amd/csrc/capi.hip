@@ -431,7 +431,26 @@ int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* pri
     s->fx_capable = true;
   if (s->p2p_capable || s->fx_capable) {
     const int64_t nm = 2LL * g.world_size * C * g.stride * g.units_per_rank;
-    CLV_HIPC(dalloc(&s->d_mail, nm));
+    // The mail is written by OTHER GPUs (system-scope write-through stores over xGMI) while this
+    // GPU polls it.  Uncached device memory (MTYPE UC: every access of every agent goes to memory,
+    // no L2 line of this GPU can hold a stale copy of a peer's store); fine-grained, then plain
+    // device memory if the allocator refuses (CLV_MAIL_ALLOC = uncached | fine | default selects)
+    {
+      const char* env = std::getenv("CLV_MAIL_ALLOC");
+      const std::string want = env ? env : "uncached";
+      const unsigned flags[3] = {hipDeviceMallocUncached, hipDeviceMallocFinegrained, hipDeviceMallocDefault};
+      const int first = want == "fine" ? 1 : want == "default" ? 2 : 0;
+      for (int k = first; k < 3 && !s->d_mail; ++k) {
+        void* p = nullptr;
+        if (hipExtMallocWithFlags(&p, sizeof(double) * (size_t)nm, flags[k]) == hipSuccess && p) {
+          s->d_mail = (double*)p;
+          s->mail_kind = k;
+        } else {
+          (void)hipGetLastError();
+        }
+      }
+      if (!s->d_mail) return cleanup_fail(fail(CLV_ENOMEM, "peer mail buffer"));
+    }
     CLV_HIPC(hipMemsetAsync(s->d_mail, 0xFF, sizeof(double) * nm, s->stream));  // every slot empty
     CLV_HIPC(dalloc(&s->d_peers, g.world_size));
   }
@@ -685,6 +704,7 @@ int clv_p2p_info(const clv_sampler* s, int64_t* out) {
   out[1] = s->p2p_ready ? 1 : 0;
   out[2] = s->d_mail ? (int64_t)sizeof(double) * 2 * s->g.world_size * s->g.n_chains * s->g.stride * s->g.units_per_rank : 0;
   out[3] = (int64_t)(uintptr_t)s->d_mail;
+  out[5] = s->d_mail ? s->mail_kind : -1;
   return CLV_OK;
 }
 
@@ -733,6 +753,27 @@ int clv_p2p_connect(clv_sampler* s, const void* handles, const uint64_t* ptrs) {
   CLV_HIP(hipMemcpy(s->d_peers, peers.data(), sizeof(double*) * W, hipMemcpyHostToDevice));
   CLV_HIP(hipStreamSynchronize(s->stream));  // the mail's sentinel fill has landed
   s->p2p_ready = true;
+  return CLV_OK;
+}
+
+int clv_p2p_disconnect(clv_sampler* s) {
+  if (!s) return fail(CLV_EINVAL, "null sampler");
+  CLV_HIP(hipSetDevice(s->device));
+  CLV_HIP(hipStreamSynchronize(s->stream));
+  s->p2p_ready = false;
+  for (void* p : s->ipc_opened) (void)hipIpcCloseMemHandle(p);
+  s->ipc_opened.clear();
+  if (s->d_peers) CLV_HIP(hipMemset(s->d_peers, 0, sizeof(double*) * s->g.world_size));
+  return CLV_OK;
+}
+
+int clv_set_wait_timeout(clv_sampler* s, double ms) {
+  if (!s || !(ms >= 1.0) || ms > 3.6e6) return fail(CLV_EINVAL, "wait timeout must be in [1 ms, 1 h]");
+  s->wait_ticks = (uint64_t)(ms * 1e5);  // s_memrealtime: 100 MHz
+  if (s->graph_exec) {  // captured with the previous bound (kernel arguments)
+    CLV_HIP(hipGraphExecDestroy(s->graph_exec));
+    s->graph_exec = nullptr;
+  }
   return CLV_OK;
 }
 

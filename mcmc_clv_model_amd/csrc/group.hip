@@ -19,6 +19,7 @@
 // redone through the copy exchange, which the group keeps from then on.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -33,6 +34,7 @@ struct clv_group {
   std::vector<double*> gathered;          // [shard][parity] -> [world][nd] on the shard's device
   std::vector<hipEvent_t> ev;             // [shard] "this shard's partials pushed" (per exchange)
   int64_t n_exchanges = 0;                // exchanges so far (their parity alternates)
+  std::vector<clv_sampler*> connected;    // shards this group connected (disconnected again by destroy)
 };
 
 namespace {
@@ -83,8 +85,16 @@ int run_copy(clv_group* G, int64_t n_sweeps) {
 int run_p2p(clv_group* G, int64_t n_sweeps) {
   const int W = (int)G->shards.size();
   std::vector<int> rc(W, CLV_OK);
+  // test hook: CLV_TEST_P2P_STALL_RANK=r leaves shard r's launch out (a shard that never runs), so
+  // the others wait out their bound and the group takes the fallback below (tests/test_gpu_multidevice)
+  const char* stall_env = std::getenv("CLV_TEST_P2P_STALL_RANK");
+  const int stall = stall_env ? std::atoi(stall_env) : -1;
   for (int r = 0; r < W; ++r) {  // every launch in flight first (each waits for the others' units)
     clv_sampler* s = G->shards[r];
+    if (r == stall) {
+      rc[r] = fail(CLV_EHIP, "test hook: shard launch withheld (CLV_TEST_P2P_STALL_RANK)");
+      continue;
+    }
     if (hipSetDevice(s->device) != hipSuccess) {
       rc[r] = fail(CLV_EHIP, "hipSetDevice");
       continue;
@@ -109,6 +119,8 @@ int run_p2p(clv_group* G, int64_t n_sweeps) {
       if (e) return e;
     }
   G->exchange = CLV_EXCHANGE_COPY;
+  for (clv_sampler* s : G->connected) (void)clv_p2p_disconnect(s);  // no shard keeps stale peer pointers
+  G->connected.clear();
   return run_copy(G, n_sweeps);
 }
 
@@ -159,6 +171,14 @@ int clv_group_create(clv_sampler* const* shards, int32_t n, int32_t exchange, cl
   // the other's memory (P2P stores from the level-2 workgroups)
   bool p2p = exchange != CLV_EXCHANGE_COPY && n > 1;
   for (int r = 0; r < n && p2p; ++r) p2p = shards[r]->p2p_capable;
+  // shards sharing a device: their persistent kernels must run at the same time from different
+  // streams, which HIP does not promise (more streams than hardware queues share a queue and then
+  // run one after another: the first would wait out its bound for mail the second never sends).
+  // AUTO takes the copy exchange there; CLV_EXCHANGE_P2P still tries it (and falls back if a wait
+  // times out).
+  for (int r = 0; r < n && p2p && exchange == CLV_EXCHANGE_AUTO; ++r)
+    for (int q = 0; q < r && p2p; ++q)
+      if (shards[q]->device == shards[r]->device) p2p = false;
   for (int r = 0; r < n && p2p; ++r) {  // shards sharing a device: their grids together
     int64_t wgs = 0;
     for (int q = 0; q < n; ++q)
@@ -186,7 +206,8 @@ int clv_group_create(clv_sampler* const* shards, int32_t n, int32_t exchange, cl
     for (int r = 0; r < n; ++r) ptrs[r] = (uint64_t)(uintptr_t)shards[r]->d_mail;
     for (int r = 0; r < n; ++r) {
       int rc = clv_p2p_connect(shards[r], nullptr, ptrs.data());
-      if (rc) return cleanup(rc);
+      if (rc) return cleanup(rc);  // (destroy disconnects the shards connected so far)
+      G->connected.push_back(shards[r]);
     }
     G->exchange = CLV_EXCHANGE_P2P;
   } else {
@@ -219,6 +240,9 @@ int32_t clv_group_exchange(const clv_group* G) { return G ? G->exchange : -1; }
 
 void clv_group_destroy(clv_group* G) {
   if (!G) return;
+  // shards outlive the group: none may keep pointers into another shard's mail (a later clv_run
+  // would fail with CLV_ESTATE instead of storing into memory that may be freed)
+  for (clv_sampler* s : G->connected) (void)clv_p2p_disconnect(s);
   for (size_t q = 0; q < G->shards.size(); ++q) {
     (void)hipSetDevice(G->shards[q]->device);
     (void)hipStreamSynchronize(G->shards[q]->stream);

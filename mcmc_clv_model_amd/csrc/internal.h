@@ -98,6 +98,7 @@ struct clv_sampler {
   bool fx_capable = false;          // fused peer exchange (launch-per-sweep, any shard size)
   bool p2p_ready = false;           // clv_p2p_connect done: clv_run runs persist_kernel
   double* d_mail = nullptr;         // [2][world][chain][units_per_rank][stride]
+  int mail_kind = -1;               // the mail's memory: 0 uncached, 1 fine-grained, 2 plain device memory
   double** d_peers = nullptr;       // [world] mail pointers (peers' opened IPC mappings, own d_mail)
   int32_t* d_wgmap = nullptr;       // persistent grid: linear workgroup -> (chain << 16 | block)
   std::vector<void*> ipc_opened;    // hipIpcOpenMemHandle mappings to close

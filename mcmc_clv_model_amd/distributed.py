@@ -30,6 +30,13 @@ import numpy as np
 from . import _lib
 
 BLOCK = _lib.BLOCK
+VERIFY_WAIT_MS = 500.0  # in-kernel wait bound while the peer exchange is checked against RCCL
+
+
+def run_wait_ms() -> float:
+    """The wait bound afterwards: clv_create's default with peers (10 s) or CLV_WAIT_TIMEOUT_MS."""
+    import os
+    return float(os.environ.get("CLV_WAIT_TIMEOUT_MS", "10000"))
 
 
 def default_blocks_per_unit(n_global: int) -> int:
@@ -204,12 +211,18 @@ class ShardedSampler:
             self.s.set_state(*snap, n0)
             dist.barrier(group=self.group)
             err = None
+            # the ranks leave the barrier together, so the check's launches start within
+            # milliseconds of each other: a short wait bound makes a failed check cost well under
+            # a second instead of the run's 10 s bound (which absorbs host-side skew later on)
+            self.s.set_wait_timeout(VERIFY_WAIT_MS)
             try:
                 self.s.run(verify_sweeps)
                 got = self.s.get_state()
                 same = all(np.array_equal(a.view(np.uint64), b.view(np.uint64)) for a, b in zip(ref, got))
             except Exception as e:  # noqa: BLE001
                 same, err = False, e
+            finally:
+                self.s.set_wait_timeout(run_wait_ms())
             if not self._all_ok(same):
                 self.s.set_state(*snap, n0)  # the RCCL path carries on from the same state
                 if required:

@@ -118,8 +118,12 @@ def resolve_seed(seed: Optional[int]) -> int:
     seed = int(seed)
     if seed < 0:  # numpy: default_rng(seed + ch) with a negative seed raises (bi:486)
         raise ValueError("expected non-negative integer")
-    if seed >= 1 << 64:
-        raise ValueError("seed must fit 64 bits (the Philox key)")
+    if seed >= 1 << 63:
+        # numpy accepts any non-negative int (default_rng(seed + ch), bi:486); the Philox key holds
+        # 64 bits, so a larger seed is folded to 63 bits deterministically through numpy's own
+        # SeedSequence hash (chain c then keys on the folded seed + c)
+        w = np.random.SeedSequence(seed).generate_state(2, np.uint32)
+        return (int(w[0]) | (int(w[1]) << 32)) & ((1 << 63) - 1)
     return seed
 
 
@@ -241,10 +245,10 @@ class HipSampler:
     def p2p_info(self) -> dict:
         """clv_p2p_info: peer exchange possible / connected, the mail buffer, and whether clv_run
         runs it in one persistent launch (else one fused sweep launch per sweep)."""
-        out = (ctypes.c_int64 * 5)()
+        out = (ctypes.c_int64 * 6)()
         check(self._L.clv_p2p_info(self.h, out))
         return dict(capable=bool(out[0]), connected=bool(out[1]), mail_bytes=int(out[2]), mail_ptr=int(out[3]),
-                    persistent=bool(out[4]))
+                    persistent=bool(out[4]), mail_memory={0: "uncached", 1: "fine-grained", 2: "device"}.get(int(out[5])))
 
     def p2p_export(self) -> bytes:
         """This rank's mail buffer as a hipIpcMemHandle (bytes) for the other ranks."""
@@ -260,6 +264,14 @@ class HipSampler:
         else:
             arr = (ctypes.c_uint64 * len(ptrs))(*[int(p) for p in ptrs])
             check(self._L.clv_p2p_connect(self.h, None, arr))
+
+    def p2p_disconnect(self) -> None:
+        """clv_p2p_disconnect: forget the peers' mail (a sharded run() needs p2p_connect again)."""
+        check(self._L.clv_p2p_disconnect(self.h))
+
+    def set_wait_timeout(self, ms: float) -> None:
+        """clv_set_wait_timeout: the bound of every in-kernel wait (ms)."""
+        check(self._L.clv_set_wait_timeout(self.h, float(ms)))
 
     @property
     def sweeps_done(self) -> int:

@@ -267,7 +267,20 @@ def pack_tape(tape, n, S, D):
     return out
 
 
-def write_replay(rbi, rtri):
+SYNTH_COV_SEED = 4242  # the U(-1,1) covariate columns c1..c8 added to the abe rows of the K=5 / K=9 cases
+
+
+def with_synthetic_covariates(df, n_cov, seed=SYNTH_COV_SEED):
+    """c1..c{n_cov}: U(-1,1) covariates (the c4/c5 covariate model) on CDNOW rows."""
+    df = df.copy()
+    rng = np.random.default_rng(seed)
+    cov = rng.uniform(-1.0, 1.0, size=(len(df), n_cov))
+    for k in range(n_cov):
+        df[f"c{k + 1}"] = cov[:, k]
+    return df
+
+
+def write_replay(rbi, rtri, only_names=None):
     df = prepare(load_cbs("abe"))
     cases = [
         # name, kind, covariates, N, S, chains, seed, mcmc (all stored: burnin 0, thin 1)
@@ -275,9 +288,17 @@ def write_replay(rbi, rtri):
         ("bi_k2", "bi", ["first_sales_scaled"], 256, 20, 1, 7, 3),
         ("tri_k3", "tri", ["gender_F", "age_scaled"], 200, 20, 1, 11, 3),
         ("bi_k1_s0", "bi", [], 64, 0, 1, 3, 2),
+        # the c4 / c5 kernel instances (verdict r2 #1): bivariate K=5 (sweep_kernel_occ4<2,5>, covariates
+        # in registers) and trivariate K=9 (sweep_kernel<3,9>, covariate rows in LDS); 384 customers =
+        # one full and one half-filled 256-customer block
+        ("bi_k5", "bi", [f"c{k}" for k in range(1, 5)], 384, 20, 1, 13, 3),
+        ("tri_k9", "tri", [f"c{k}" for k in range(1, 9)], 384, 20, 1, 17, 3),
     ]
     for name, kind, covs, n, S, chains, seed, mcmc in cases:
-        sub = df.iloc[:n].copy().reset_index(drop=True)
+        if only_names and name not in only_names:
+            continue
+        base = with_synthetic_covariates(df, 8) if covs and covs[0] == "c1" else df
+        sub = base.iloc[:n].copy().reset_index(drop=True)
         kw = dict(mcmc=mcmc, burnin=0, thin=1, chains=chains, seed=seed, trace=0, n_mh_steps=S)
         fn_r = rbi.mcmc_draw_parameters if kind == "bi" else rtri.mcmc_draw_parameters_rfm_m
         fn_o = orc.mcmc_draw_parameters if kind == "bi" else orc.mcmc_draw_parameters_rfm_m
@@ -303,11 +324,35 @@ def write_replay(rbi, rtri):
 
 
 # ---------------------------------------------------------------------------------------------
+SYNTH_ENVELOPE = {  # name -> (kind, K, D, data seed): 20,000 synthetic customers (c4 / c5 model)
+    "synth_bi_k5": ("bi", 5, 2, 20251017),
+    "synth_tri_k9": ("tri", 9, 3, 20251018),
+}
+SYNTH_ENVELOPE_N = 20_000
+
+
+def synthetic_data(name):
+    """The envelope's synthetic CBS: the product's vectorised generator (mcmc_clv_model_amd/data.py,
+    plain numpy), regenerated bit for bit by the GPU test from the stored seed (sha256 checked)."""
+    from mcmc_clv_model_amd.data import synthetic_cbs
+    kind, K, D, seed = SYNTH_ENVELOPE[name]
+    return synthetic_cbs(SYNTH_ENVELOPE_N, K, D, seed=seed)
+
+
+def frame_sha256(df):
+    import hashlib
+    h = hashlib.sha256()
+    for c in df.columns:
+        h.update(c.encode())
+        h.update(np.ascontiguousarray(df[c].to_numpy()).tobytes())
+    return h.hexdigest()
+
+
 def _envelope_chain(args):
     kind, covs, seed, burnin, mcmc = args[:5]
     data = args[5] if len(args) > 5 else "abe"
     os.environ["OMP_NUM_THREADS"] = "1"
-    df = prepare(load_cbs(data))
+    df = synthetic_data(data) if data in SYNTH_ENVELOPE else prepare(load_cbs(data))
     fn = orc.mcmc_draw_parameters if kind == "bi" else orc.mcmc_draw_parameters_rfm_m
     d = fn(df, covs, mcmc=mcmc, burnin=burnin, thin=1, chains=1, seed=seed, trace=0)
     l1 = d["level_1"][0]
@@ -371,6 +416,48 @@ def write_envelope_full(rbi, rtri, M=16, burnin=1000, mcmc=1000):
         np.savez_compressed(os.path.join(HERE, f"envelope_{name}.npz"), **out)
         print("envelope", name)
     with open(os.path.join(HERE, "oracle_pin_full.json"), "w") as f:
+        json.dump(dict(reference=REF, checks=pins), f, indent=1)
+
+
+def write_envelope_synth(rbi, rtri, M=16, burnin=1000, mcmc=1000):
+    """G3 for the c4 / c5 kernel instances (verdict r2 #1): 20,000 synthetic customers of the c4
+    model (bivariate, K = 5) and the c5 model (trivariate, K = 9) — the covariate counts that select
+    sweep_kernel_occ4<2,5> and the LDS-covariate sweep_kernel<3,9> — at reduced length.  The oracle
+    is first re-pinned bitwise against the reference on these exact inputs (4 sweeps, 2 chains)."""
+    pins = []
+    names = list(SYNTH_ENVELOPE)
+    for name in names:
+        kind, K, D, dseed = SYNTH_ENVELOPE[name]
+        df = synthetic_data(name)
+        covs = [f"c{k}" for k in range(1, K)]
+        kw = dict(mcmc=2, burnin=2, thin=1, chains=2, seed=7, trace=0)
+        fn_r = rbi.mcmc_draw_parameters if kind == "bi" else rtri.mcmc_draw_parameters_rfm_m
+        fn_o = orc.mcmc_draw_parameters if kind == "bi" else orc.mcmc_draw_parameters_rfm_m
+        assert bitwise_equal(fn_r(df, covs, **kw), fn_o(df, covs, **kw)), name
+        pins.append(dict(case=name, n=len(df), covariates=covs, data_seed=dseed, sha256=frame_sha256(df), **kw,
+                         bitwise=True))
+        print("pinned", name)
+    jobs = [(SYNTH_ENVELOPE[name][0], [f"c{k}" for k in range(1, SYNTH_ENVELOPE[name][1])], 5000 + m, burnin, mcmc,
+             name) for name in names for m in range(M)]
+    with Pool(min(8, len(jobs))) as pool:  # 1 thread per process
+        res = pool.map(_envelope_chain, jobs, chunksize=1)
+    for ci, name in enumerate(names):
+        kind, K, D, dseed = SYNTH_ENVELOPE[name]
+        rs = res[ci * M:(ci + 1) * M]
+        out = dict(kind=kind, covariates=np.array([f"c{k}" for k in range(1, K)], dtype="U32"), M=M, burnin=burnin,
+                   mcmc=mcmc, data=np.array("synthetic"), data_seed=dseed, data_n=SYNTH_ENVELOPE_N, data_K=K,
+                   data_D=D, data_sha256=np.array(frame_sha256(synthetic_data(name))),
+                   seeds=np.array([5000 + m for m in range(M)]))
+        for k in rs[0][0].keys():
+            v = np.stack([r[0][k] for r in rs])
+            out[k + "_mean"] = v.mean(0)
+            out[k + "_sd"] = v.std(0, ddof=1)
+            out[k + "_chains"] = v.mean(1)
+        out["level2_median"] = np.stack([r[1] for r in rs])
+        out["loglik"] = np.array([r[2] for r in rs])
+        np.savez_compressed(os.path.join(HERE, f"envelope_{name}.npz"), **out)
+        print("envelope", name)
+    with open(os.path.join(HERE, "oracle_pin_synth.json"), "w") as f:
         json.dump(dict(reference=REF, checks=pins), f, indent=1)
 
 
@@ -503,16 +590,18 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-envelope", action="store_true")
     ap.add_argument("--only", default="")
+    ap.add_argument("--replay-names", default="", help="comma-separated subset of the replay cases")
     a = ap.parse_args()
     rbi, rtri = ref_modules()
     only = set(a.only.split(",")) if a.only else None
     steps = [("pin", lambda: pin_oracle(rbi, rtri)), ("data", write_data), ("philox", write_philox_kat),
-             ("formulas", lambda: write_formulas(rbi, rtri)), ("replay", lambda: write_replay(rbi, rtri)),
+             ("formulas", lambda: write_formulas(rbi, rtri)), ("replay", lambda: write_replay(rbi, rtri, set(a.replay_names.split(",")) if a.replay_names else None)),
              ("published", write_published), ("analysis", lambda: write_analysis(rbi, rtri)),
              ("dataprep", lambda: write_dataprep(rbi))]
     if not a.skip_envelope:
         steps.append(("envelope", write_envelope))
         steps.append(("envelope_full", lambda: write_envelope_full(rbi, rtri)))
+        steps.append(("envelope_synth", lambda: write_envelope_synth(rbi, rtri)))
     for name, fn in steps:
         if only is None or name in only:
             fn()

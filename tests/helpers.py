@@ -26,6 +26,15 @@ def cdnow(name: str = "abe", n: int | None = None) -> pd.DataFrame:
     return df
 
 
+def with_covariates(df: pd.DataFrame, n_cov: int, seed: int = 4242) -> pd.DataFrame:
+    """c1..c{n_cov}: U(-1,1) covariate columns (the c4/c5 covariate model) added to a CBS."""
+    df = df.copy()
+    cov = np.random.default_rng(seed).uniform(-1.0, 1.0, size=(len(df), n_cov))
+    for k in range(n_cov):
+        df[f"c{k + 1}"] = cov[:, k]
+    return df
+
+
 def replay_case(name: str):
     """(DataFrame, covariates, fixture) of a G2 replay fixture."""
     f = golden(f"replay_{name}.npz")

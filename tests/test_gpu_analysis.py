@@ -123,6 +123,45 @@ def test_future_transactions_tri_spend(fx):
     assert np.array_equal(x, x2)
 
 
+def test_future_transactions_tri_spend_vs_reference(fx):
+    """The reference's own trivariate predictive output (analysis_abe400.npz: xstar_tri, spend_tri
+    from tri:660-749 on the fixture's draws) against ours on the SAME unmodified draws — natural-scale
+    eta passed as the lognormal log-mean, the reference's quirk (tri:733) kept.  Independent streams,
+    so in distribution:
+      * zero pattern: spend is 0 exactly where the count is 0 (both);
+      * single-transaction draws: log(spend) - eta ~ N(0, sigma_s^2) — ours vs the reference's
+        residuals, two-sample KS p > 1e-3, and each against N(0, 0.25), KS p > 1e-3;
+      * all draws with x > 0: spend / (x exp(eta + sigma_s^2 / 2)) has mean 1 for both, and the two
+        means agree within 5 two-sample standard errors;
+      * per customer, the total count over the 40 draws agrees with the reference's within 4
+        Poisson-difference sd for >= 99% of customers (the spend's count process)."""
+    from mcmc_clv_model_amd import draw_future_transactions_rfm_m
+    f, cbs, bi, tri = fx
+    x, sp = draw_future_transactions_rfm_m(cbs, tri, T_star=39.0, sigma_s=0.5, seed=29)
+    xr, spr = f["xstar_tri"], f["spend_tri"]
+    assert x.shape == xr.shape and sp.shape == spr.shape and sp.dtype == np.float64
+    eta = np.concatenate(tri["level_1"])[:, :, 4]
+    assert eta.min() > 1.0  # natural scale (the quirk): the log-mean is eta itself, not log(eta)
+    for xx, ss in ((x, sp), (xr, spr)):
+        assert (ss[xx == 0] == 0).all() and (ss[xx > 0] > 0).all() and np.isfinite(ss).all()
+    r = np.log(sp[x == 1]) - eta[x == 1]
+    rr = np.log(spr[xr == 1]) - eta[xr == 1]
+    assert min(r.size, rr.size) > 500
+    assert stats.ks_2samp(r, rr).pvalue > 1e-3
+    for v in (r, rr):
+        assert stats.kstest(v, "norm", args=(0.0, 0.5)).pvalue > 1e-3
+    ratio = sp[x > 0] / (x[x > 0] * np.exp(eta[x > 0] + 0.125))
+    ratio_r = spr[xr > 0] / (xr[xr > 0] * np.exp(eta[xr > 0] + 0.125))
+    for v in (ratio, ratio_r):
+        assert abs(v.mean() - 1.0) < 5 * v.std() / np.sqrt(v.size)
+    se = np.sqrt(ratio.var() / ratio.size + ratio_r.var() / ratio_r.size)
+    assert abs(ratio.mean() - ratio_r.mean()) < 5 * se
+    lv = np.concatenate(tri["level_1"])
+    rate = (lv[:, :, 0] * np.where(lv[:, :, 3] > 0.5, 39.0, np.clip(lv[:, :, 2] - cbs["T_cal"].to_numpy(), 0, 39.0))).sum(0)
+    z = (x.sum(0) - xr.sum(0)) / np.sqrt(np.maximum(2 * rate, 1e-9))
+    assert np.mean(np.abs(z) <= 4) >= 0.99
+
+
 def test_weekly_tracking(fx):
     """Tracking curve: one exact Poisson of the summed active rate per (draw, week) — the same
     distribution as the reference's per-customer draws.  Compared with the exact expectation and

@@ -47,10 +47,13 @@ def test_devices_chain_groups_bitwise(capsys):
 
 
 @pytest.mark.parametrize("D,sink,exchange", [(2, "full", "auto"), (3, "summary+pct", "auto"), (2, "summary", "copy"),
-                                             (3, "full", "copy")])
+                                             (3, "full", "copy"), (2, "summary", "p2p"), (3, "full", "p2p")])
 def test_devices_customer_shards_bitwise(D, sink, exchange):
-    """shard='customers': every chain's customers split over the devices, one exchange per sweep
-    (p2p: both CDNOW-size grids fit the card together; copy forced), bitwise the one-device run."""
+    """shard='customers': every chain's customers split over the devices, one exchange per sweep,
+    bitwise the one-device run.  Shards sharing a device: "auto" takes the copy exchange (the two
+    persistent kernels would have to run concurrently from two streams, which HIP does not promise);
+    "p2p" requested explicitly runs the peer stores between the two resident grids (both CDNOW-size
+    grids fit the card together) or, if a wait times out, the copy fallback — same bits either way."""
     from mcmc_clv_model_amd import mcmc_draw_parameters, mcmc_draw_parameters_rfm_m
     fn, covs = ((mcmc_draw_parameters, ["first_sales_scaled"]) if D == 2 else
                 (mcmc_draw_parameters_rfm_m, ["gender_F", "age_scaled"]))
@@ -58,8 +61,55 @@ def test_devices_customer_shards_bitwise(D, sink, exchange):
     kw = dict(mcmc=21, burnin=9, thin=3, chains=2, seed=9, trace=0, draw_sink=sink)
     one = fn(df, covs, **kw)
     two = fn(df, covs, devices=[0, 0], shard="customers", exchange=exchange, **kw)
-    assert two.pop("exchange") == ("p2p" if exchange == "auto" else "copy")
+    ex = two.pop("exchange")
+    assert ex == "copy" if exchange != "p2p" else ex in ("p2p", "copy")
     _same(one, two)
+
+
+def test_group_p2p_timeout_falls_back_to_copy(monkeypatch):
+    """the group-level fallback.  A shard whose persistent launch never runs (test hook
+    CLV_TEST_P2P_STALL_RANK=1) leaves shard 0 waiting for its mail: the wait bound (300 ms here)
+    expires, shard 0 keeps its state, the group redoes the call through the copy exchange and keeps
+    it — results bitwise the unsharded run, clv_group_exchange reports copy, and after the group is
+    destroyed no shard is left connected."""
+    from mcmc_clv_model_amd.sampler import HipGroup, HipSampler, build_problem, make_prior
+    from mcmc_clv_model_amd import distributed as Dm
+    df = cdnow("full")
+    p = build_problem(df, ["first_sales_scaled"], 2)
+    kw = dict(mcmc=6, burnin=4, thin=2, chains=2, seed=17, draw_sink="summary")
+    with HipSampler(p, **kw) as s:
+        s.run(10)
+        ref = s.get_state()
+        ref_sums, _ = s.read_summary()
+    monkeypatch.setenv("CLV_WAIT_TIMEOUT_MS", "300")
+    plan = Dm.plan(p.N, 2)
+    prior = make_prior(p, p.N)
+    shards = []
+    for r in range(2):
+        b, e = plan.shard(r)
+        shards.append(HipSampler(Dm.slice_problem(p, b, e), n_global=p.N, shard_begin=r * plan.blocks_per_rank * 256,
+                                 world_size=2, rank=r, blocks_per_rank=plan.blocks_per_rank,
+                                 blocks_per_unit=plan.blocks_per_unit, prior=prior, device=0, **kw))
+    try:
+        g = HipGroup(shards, "p2p")
+        assert g.exchange == "p2p" and all(sh.p2p_info()["connected"] for sh in shards)
+        monkeypatch.setenv("CLV_TEST_P2P_STALL_RANK", "1")
+        g.run(10)
+        monkeypatch.delenv("CLV_TEST_P2P_STALL_RANK")
+        assert g.exchange == "copy"
+        assert not any(sh.p2p_info()["connected"] for sh in shards)
+        g.close()
+        for r, sh in enumerate(shards):
+            b, e = plan.shard(r)
+            lam, mu, beta, sigma = sh.get_state()
+            assert np.array_equal(bits(lam), bits(ref[0][:, b:e])) and np.array_equal(bits(mu), bits(ref[1][:, b:e]))
+            assert np.array_equal(bits(beta), bits(ref[2])) and np.array_equal(bits(sigma), bits(ref[3]))
+            sums, _ = sh.read_summary()
+            assert np.array_equal(bits(sums), bits(ref_sums[:, :, b:e]))
+            assert sh.p2p_info()["mail_memory"] in ("uncached", "fine-grained", "device")
+    finally:
+        for sh in shards:
+            sh.close()
 
 
 def test_devices_customer_shards_large_units_copy():

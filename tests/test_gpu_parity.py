@@ -9,7 +9,7 @@ import pandas as pd
 import pytest
 
 from oracle import philox as oph
-from tests.helpers import GOLDEN, bits, cdnow, golden, replay_case
+from tests.helpers import GOLDEN, bits, cdnow, golden, replay_case, with_covariates
 
 pytestmark = pytest.mark.gpu
 
@@ -126,13 +126,16 @@ def _replay_run(name):
     return d, f
 
 
-@pytest.mark.parametrize("name", ["bi_k1", "bi_k2", "tri_k3", "bi_k1_s0"])
+@pytest.mark.parametrize("name", ["bi_k1", "bi_k2", "tri_k3", "bi_k1_s0", "bi_k5", "tri_k9"])
 def test_replay_trajectory_matches_reference(L, name):
     """G2: the HIP sampler consuming the reference's own variates reproduces the reference's
     trajectory (every sweep stored): lambda, mu, tau, eta and level-2 draws <= 1e-12 rel
     (1e-10 for the level-2 record, whose S_n is summed in a different order), z exact, and the
     marginal log-likelihood <= 1e-12 rel.  At most 0.5% of customers may differ (borderline
-    accept flips from 1-ulp exp/log differences — none expected in 3 sweeps)."""
+    accept flips from 1-ulp exp/log differences — none expected in 3 sweeps).
+    bi_k5 / tri_k9 run the c4 / c5 kernel instances' covariate handling (X @ beta of bi:284,
+    tri:403, tri:321 and X'Y): sweep_kernel_occ4<2,5> with the covariate row in registers and
+    sweep_kernel<3,9> with it in LDS (Cust<3,9,CL=true>), on 384 customers (a half-filled block)."""
     d, f = _replay_run(name)
     l1 = np.stack(d["level_1"])
     ref = f["level_1"]
@@ -499,7 +502,9 @@ def _run_mode(p, persistent, sweeps, chunks, **kw):
                                              (3, ["gender_F", "age_scaled"], 23570, "summary", 20),
                                              (2, [], 1000, "full", 20), (3, ["gender_F"], 300, "full", 20),
                                              (2, ["first_sales_scaled"], 2357, "full", 7),
-                                             (3, ["gender_F"], 2357, "summary", 23)])
+                                             (3, ["gender_F"], 2357, "summary", 23),
+                                             (2, [f"c{k}" for k in range(1, 5)], 3000, "summary", 20),
+                                             (3, [f"c{k}" for k in range(1, 9)], 2357, "full", 20)])
 def test_persistent_kernel_bitwise_equals_launch_per_sweep(L, D, covs, n, sink, S):
     """World size 1: the persistent kernel (one launch for all of a clv_run's sweeps, sentinel-slot
     hand-off to a level-2 workgroup per chain) is chosen by default where the grid fits at once,
@@ -507,8 +512,12 @@ def test_persistent_kernel_bitwise_equals_launch_per_sweep(L, D, covs, n, sink, 
     level-2 records, log-likelihood, summaries — across clv_run calls of uneven length (the
     carried state at each launch boundary), burn-in and thinning; S = 7 (a partial last chunk of
     drawn-ahead variates) and S = 23 (more steps than the drawn-ahead registers hold: variates
-    drawn within the sweep)."""
+    drawn within the sweep).  K = 5 (bivariate) and K = 9 (trivariate) compare the persistent
+    kernel's register-resident covariate rows with the c4 / c5 launch-per-sweep instances
+    (sweep_kernel_occ4<2,5>; sweep_kernel<3,9> with the covariate rows in LDS)."""
     df = cdnow("full", n) if n > 2357 else cdnow("abe", n)
+    if covs and covs[0] == "c1":
+        df = with_covariates(df, len(covs))
     from mcmc_clv_model_amd.sampler import build_problem
     p = build_problem(df, covs, D)
     kw = dict(mcmc=25, burnin=6, thin=3, chains=3, seed=2024, draw_sink=sink, n_mh_steps=S)

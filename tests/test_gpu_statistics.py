@@ -27,8 +27,14 @@ def _run_envelope(name, M=16, seed=777):
     fn = mcmc_draw_parameters if str(f["kind"]) == "bi" else mcmc_draw_parameters_rfm_m
     data = str(f["data"]) if "data" in f.files else "abe"
     kw = dict(mcmc=int(f["mcmc"]), burnin=int(f["burnin"]), thin=1, chains=M, seed=seed, trace=0)
-    if data == "full":  # 23,570 customers: the on-device running means (summary sink), no level-1 D2H
-        d = fn(cdnow("full"), covs, draw_sink="summary", **kw)
+    if data in ("full", "synthetic"):  # 20k+ customers: the on-device running means (summary sink)
+        if data == "synthetic":
+            from mcmc_clv_model_amd.data import synthetic_cbs
+            df = synthetic_cbs(int(f["data_n"]), int(f["data_K"]), int(f["data_D"]), seed=int(f["data_seed"]))
+            assert frame_sha256(df) == str(f["data_sha256"]), "synthetic envelope data differ from the fixture's"
+        else:
+            df = cdnow("full")
+        d = fn(df, covs, draw_sink="summary", **kw)
         sm = d["summary"]
         assert sm["n_draws"] == int(f["mcmc"])
         st = dict(log_lambda=sm["log_lambda"], log_mu=sm["log_mu"], p_alive=sm["z"], lam=sm["lambda"])
@@ -47,7 +53,17 @@ def _run_envelope(name, M=16, seed=777):
     return f, {k: np.stack(v) for k, v in stats.items() if v}, d
 
 
-@pytest.mark.parametrize("name", ["c1_bi_k1", "abe_bi_k2", "abe_tri_k3", "full_bi_k2", "full_tri_k3"])
+def frame_sha256(df):
+    import hashlib
+    h = hashlib.sha256()
+    for c in df.columns:
+        h.update(c.encode())
+        h.update(np.ascontiguousarray(df[c].to_numpy()).tobytes())
+    return h.hexdigest()
+
+
+@pytest.mark.parametrize("name", ["c1_bi_k1", "abe_bi_k2", "abe_tri_k3", "full_bi_k2", "full_tri_k3",
+                                  "synth_bi_k5", "synth_tri_k9"])
 def test_posterior_envelope_vs_reference_ensemble(name):
     """Population means within 4 standard errors of the chain-to-chain spread (the common shift of
     every customer that the slowly mixing hyper-parameters cause); per customer, after that common
@@ -63,7 +79,10 @@ def test_posterior_envelope_vs_reference_ensemble(name):
     full_bi_k2 / full_tri_k3 are c2 and c3 (full CDNOW, 23,570 customers, their covariates) at
     reduced length (1000 + 1000 sweeps; oracle re-pinned bitwise to the reference on these exact
     inputs, oracle_pin_full.json); the GPU side keeps its per-customer means on device (summary
-    sink) — the production path of the 1M/10M configurations."""
+    sink) — the production path of the 1M/10M configurations.  synth_bi_k5 / synth_tri_k9 are the
+    c4 / c5 models (U(-1,1) covariates, K = 5 bivariate, K = 9 trivariate) on 20,000
+    synthetic customers at the same reduced length — the covariate counts that select the c4 / c5
+    kernel instances (oracle re-pinned bitwise on these inputs, oracle_pin_synth.json)."""
     f, g, d = _run_envelope(name)
     M_ref = int(f["M"])
     for k, v in g.items():

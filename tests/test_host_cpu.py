@@ -61,6 +61,19 @@ def test_validation_errors_before_device():
         mcmc_draw_parameters(df, ["nope"])
 
 
+def test_seed_resolution():
+    """seed + chain keys the chain (bi:486); numpy accepts any non-negative int, so seeds beyond the
+    64-bit Philox key are folded deterministically (SeedSequence hash), never rejected."""
+    from mcmc_clv_model_amd.sampler import resolve_seed
+    assert resolve_seed(42) == 42 and resolve_seed(0) == 0 and resolve_seed((1 << 63) - 1) == (1 << 63) - 1
+    big = [resolve_seed(v) for v in (1 << 63, 1 << 64, 3 ** 200, 3 ** 200 + 1)]
+    assert big == [resolve_seed(v) for v in (1 << 63, 1 << 64, 3 ** 200, 3 ** 200 + 1)]  # deterministic
+    assert len(set(big)) == 4 and all(0 <= v < (1 << 63) for v in big)
+    with pytest.raises(ValueError):
+        resolve_seed(-1)
+    assert 0 <= resolve_seed(None) < (1 << 63)
+
+
 def test_no_cpu_fallback_without_gpu():
     """The product path raises instead of silently running on the CPU."""
     from mcmc_clv_model_amd import _lib, mcmc_draw_parameters

@@ -14,6 +14,25 @@ from tests.helpers import GOLDEN, bits, cdnow, golden, replay_case
 def test_oracle_pin_record_all_bitwise():
     pin = json.load(open(os.path.join(GOLDEN, "oracle_pin.json")))
     assert pin["checks"] and all(c["bitwise_equal"] for c in pin["checks"])
+    for name in ("oracle_pin_full.json", "oracle_pin_synth.json"):  # c2/c3 inputs; c4/c5-model inputs
+        pin = json.load(open(os.path.join(GOLDEN, name)))
+        assert pin["checks"] and all(c["bitwise"] for c in pin["checks"])
+
+
+@pytest.mark.parametrize("name", ["synth_bi_k5", "synth_tri_k9"])
+def test_synthetic_envelope_inputs_regenerate(name):
+    """The c4/c5-model envelope fixtures store the generator seed, not the data: the product's
+    generator (mcmc_clv_model_amd/data.py, numpy) must regenerate the exact inputs the oracle ran on."""
+    import hashlib
+    from mcmc_clv_model_amd.data import synthetic_cbs
+    f = golden(f"envelope_{name}.npz")
+    df = synthetic_cbs(int(f["data_n"]), int(f["data_K"]), int(f["data_D"]), seed=int(f["data_seed"]))
+    h = hashlib.sha256()
+    for c in df.columns:
+        h.update(c.encode())
+        h.update(np.ascontiguousarray(df[c].to_numpy()).tobytes())
+    assert h.hexdigest() == str(f["data_sha256"])
+    assert f["log_lambda_mean"].shape == (int(f["data_n"]),) and int(f["M"]) == 16
 
 
 def test_reference_smoke_bi553_reproduced_bitwise():
@@ -99,7 +118,7 @@ def test_formulas_draw_eta():
     assert np.array_equal(bits(post_mean + np.sqrt(post_var) * f["eta_z"]), bits(f["eta_out"]))
 
 
-@pytest.mark.parametrize("name", ["bi_k1", "bi_k2", "tri_k3", "bi_k1_s0"])
+@pytest.mark.parametrize("name", ["bi_k1", "bi_k2", "tri_k3", "bi_k1_s0", "bi_k5", "tri_k9"])
 def test_oracle_replay_fixtures_bitwise(name):
     """The oracle regenerates the reference's recorded outputs exactly (fixture = reference run)."""
     df, covs, f = replay_case(name)
