@@ -170,7 +170,7 @@ def cpu_baseline_child(workload: str, warm: int, timed: int) -> None:
     print(json.dumps(dict(s_per_sweep=dt / timed, value=len(df) * timed / dt)))
 
 
-def cpu_baseline(workload: str, warm: int = 20, timed: int = 200):
+def cpu_baseline(workload: str, warm: int = 20, timed: int = 200, parallel: bool = True):
     if WORKLOADS[workload][1].startswith("synthetic:"):  # ~3 s/sweep on one core
         warm, timed = 2, 5
     env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1",
@@ -184,6 +184,8 @@ def cpu_baseline(workload: str, warm: int = 20, timed: int = 200):
                s_per_sweep=r["s_per_sweep"],
                sample=f"oracle/ref_cpu.py (numpy restatement, bitwise equal to the reference) on {workload}: "
                       f"1 chain x {n} customers, {timed} timed sweeps after {warm} warm-up sweeps, 1 thread")
+    if not parallel:
+        return res
     # also an all-cores throughput — P independent single-threaded chains in P
     # processes at once (the reference runs its chains sequentially; this is its best case)
     procs = min(16, os.cpu_count() or 1)  # the GPU box's CPU share is 16 (gpurun)
@@ -250,8 +252,10 @@ def measure_config(name: str, world: int, rank: int, local_rank: int, dist, step
     K = len(covs) + 1
     value = chains * n_total * steps / dt
     bpu = algorithmic_bytes(D, K, stored_fraction(burnin, thin, warmup + 1, warmup + steps), sink)
-    return dict(workload=f"{name}: {'bivariate' if D == 2 else 'trivariate'}, K={K}, synthetic "
-                         f"(mcmc_clv_model_amd.data.synthetic_cbs)",
+    data = WORKLOADS[name][1]
+    return dict(workload=f"{name}: {'bivariate' if D == 2 else 'trivariate'}, K={K}, " +
+                         ("synthetic (mcmc_clv_model_amd.data.synthetic_cbs)" if data.startswith("synthetic:") else
+                          f"CDNOW {data} CBS"),
                 scaling="strong" if name == "c4" else "weak", value=value, unit="customer-sweeps/s",
                 n_customers=n_total, customers_per_gpu=n_total // world, chains=chains, steps=steps, warmup=warmup,
                 ms_per_step=dt / steps * 1e3, draw_sink=sink,
@@ -284,6 +288,8 @@ def main():
                     help="BASELINE multi-GPU configurations also measured at this N (c4 strong, c5 weak "
                          "scaling), reported under `configs`; '' to skip")
     ap.add_argument("--scaling-steps", type=int, default=200)
+    ap.add_argument("--no-c1-leg", dest="c1_leg", action="store_false",
+                    help="skip BASELINE configs[0] (c1 on the GPU and its 1-core CPU leg)")
     ap.add_argument("--one-gpu-rehearsal", action="store_true",
                     help="world size > 1 on a one-GPU box: every rank on device 0, gloo process group (the "
                          "exchange paths are exercised; the numbers are not a scaling measurement)")
@@ -447,10 +453,22 @@ def main():
         extra[name] = measure_config(name, world, rank, local_rank, dist, a.scaling_steps, 80, a.graph_chunk,
                                      a.exchange if world > 1 else "rccl")
 
+    if world == 1 and not a.force_sharded and a.c1_leg:
+        # BASELINE configs[0] ("Bivariate M1, Abe 1/10 CDNOW subset, 4000 iters on CPU numpy reference
+        # path"): the same 4-chain c1 sampler on the GPU (2,000 sweeps after 80), next to its 1-core
+        # CPU leg in cpu_baseline["c1"]
+        extra["c1"] = measure_config("c1", 1, rank, local_rank, None, 2000, 80, 0, "rccl")
+
     if rank == 0:
         cpu = None
         if world == 1 and not a.no_cpu_baseline and not a.force_sharded:
             cpu = cpu_baseline(a.workload)
+            if a.c1_leg and a.workload != "c1":
+                c1 = cpu_baseline("c1", parallel=False)
+                cpu["c1"] = dict(value=c1["value"], unit=c1["unit"], cores=1, kind=c1["kind"],
+                                 s_per_sweep=c1["s_per_sweep"], sample=c1["sample"],
+                                 gpu_value=extra["c1"]["value"] if "c1" in extra else None,
+                                 gpu_speedup=(extra["c1"]["value"] / c1["value"]) if "c1" in extra else None)
         wl = WORKLOADS[a.workload]
         line = dict(
             metric="MCMC sweeps/sec x N_customers (customer-sweeps/s)", value=value, unit="customer-sweeps/s",

@@ -255,6 +255,9 @@ int clv_debug_mh_step(int64_t n, const int32_t* x, const uint8_t* z, const doubl
 /* Host only (no device): the persistent grid's placement map for n_chains chains of nb customer
  * workgroups (+1 level-2 workgroup each) on n_cu CUs — out[linear workgroup] = chain << 16 | block. */
 int clv_debug_wg_map(int32_t n_chains, int32_t nb, int32_t n_cu, int32_t* out);
+/* Host only: 1 if a persistent grid of grid_wgs workgroups is taken as resident at once on n_cu CUs
+ * admitting blocks_per_cu of them each (the occupancy answer less a 5% residency margin), else 0. */
+int clv_debug_persist_fits(int64_t grid_wgs, int32_t blocks_per_cu, int32_t n_cu);
 
 /* ---- In-process multi-device runs (SURVEY.md §8b devices=, §8e) ----
  * A group drives the n shards of one problem from one host thread: shards[r] = the sampler of rank

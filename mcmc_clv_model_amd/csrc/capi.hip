@@ -231,7 +231,21 @@ int64_t clv_replay_sweep_stride(const clv_sampler* s) {
 
 }  // extern "C"
 
+// The persistent kernels spin on other workgroups of their grid, so every workgroup must be
+// resident at once.  The occupancy API's answer can be one block per CU high near an SGPR edge
+// (MI355X guide, "Residency and cooperative launch": admitted blocks per CU = min(API, 8,
+// floor(800 / (ceil(sgpr/16)*16 + 16))) for 256-thread blocks), and another kernel of the process
+// may hold slots too: a grid is taken as fitting only with a margin of 5% of the slots (at least
+// one per 32 CUs).  c2 / c3: 376 of 512 slots; c4 at 8 ranks (497 of 512) goes to the fused
+// exchange instead.  Every wait is bounded regardless.
+bool clv::persist_grid_fits(int64_t grid_wgs, int blocks_per_cu, int n_cu) {
+  const int64_t slots = (int64_t)blocks_per_cu * n_cu;
+  const int64_t margin = std::max<int64_t>(n_cu / 32, (slots + 19) / 20);
+  return grid_wgs > 0 && slots > 0 && grid_wgs <= slots - margin;
+}
+
 namespace {
+
 // Persistent grid: which (chain, block) each dispatched workgroup runs.  The grid has more
 // workgroups (T = chains x (blocks + 1)) than CUs, and the dispatcher fills every CU once before
 // doubling up: linear workgroup i < T - n_cu shares its CU with workgroup i + n_cu (measured,
@@ -409,7 +423,7 @@ int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* pri
     if (persist_occupancy(g.D, g.K, false, &s->persist_bpc) == hipSuccess &&
         hipGetDeviceProperties(&prop, s->device) == hipSuccess)
       s->n_cu = prop.multiProcessorCount;
-    if ((!env || std::string(env) != "0") && (int64_t)s->persist_bpc * s->n_cu >= (int64_t)(nb_local + 1) * C)
+    if ((!env || std::string(env) != "0") && persist_grid_fits((int64_t)(nb_local + 1) * C, s->persist_bpc, s->n_cu))
       s->persistent = true;
   }
   // World size > 1: the same persistent kernel exchanging unit partials with its peers over xGMI
@@ -422,7 +436,7 @@ int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* pri
         hipGetDeviceProperties(&prop, s->device) == hipSuccess)
       s->n_cu = prop.multiProcessorCount;
     const char* env = std::getenv("CLV_PERSISTENT");  // "0": the fused exchange below instead
-    if ((!env || std::string(env) != "0") && (int64_t)s->persist_bpc * s->n_cu >= (int64_t)(nb_local + 1) * C)
+    if ((!env || std::string(env) != "0") && persist_grid_fits((int64_t)(nb_local + 1) * C, s->persist_bpc, s->n_cu))
       s->p2p_capable = true;
   }
   // Any other shard: the sweep kernel's fused level-2 tail exchanges through the same mail (one
@@ -1245,6 +1259,10 @@ int clv_debug_hyper_variates(uint64_t seed, int32_t chain, uint32_t sweep, doubl
   CLV_HIP(hipFree(dc));
   CLV_HIP(hipFree(dn));
   return CLV_OK;
+}
+
+int clv_debug_persist_fits(int64_t grid_wgs, int32_t blocks_per_cu, int32_t n_cu) {
+  return persist_grid_fits(grid_wgs, blocks_per_cu, n_cu) ? 1 : 0;
 }
 
 int clv_debug_wg_map(int32_t n_chains, int32_t nb, int32_t n_cu, int32_t* out) {

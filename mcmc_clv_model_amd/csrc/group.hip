@@ -183,7 +183,7 @@ int clv_group_create(clv_sampler* const* shards, int32_t n, int32_t exchange, cl
     int64_t wgs = 0;
     for (int q = 0; q < n; ++q)
       if (shards[q]->device == shards[r]->device) wgs += (int64_t)(shards[q]->g.nb_local + 1) * shards[q]->g.n_chains;
-    p2p = wgs <= (int64_t)shards[r]->persist_bpc * shards[r]->n_cu;
+    p2p = persist_grid_fits(wgs, shards[r]->persist_bpc, shards[r]->n_cu);
   }
   for (int r = 0; r < n && p2p; ++r)
     for (int q = 0; q < n && p2p; ++q) {

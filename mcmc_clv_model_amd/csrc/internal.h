@@ -17,6 +17,9 @@ int fail(int code, const std::string& msg);
 // its carried state (or restore the state it started from, if a wait in it timed out).
 int persist_launch(clv_sampler* s, int64_t n_sweeps);
 int persist_wait(clv_sampler* s);
+// A persistent grid of grid_wgs workgroups fits at once (with a residency margin) on n_cu CUs
+// admitting blocks_per_cu of its workgroups each (capi.hip).
+bool persist_grid_fits(int64_t grid_wgs, int blocks_per_cu, int n_cu);
 
 template <class T>
 hipError_t dalloc(T** p, size_t count) {

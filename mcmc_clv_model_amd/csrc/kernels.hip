@@ -2282,12 +2282,32 @@ __global__ void debug_variates_kernel(uint64_t seed, int chain, uint32_t sweep, 
   ea[i] = -log_fast(u53_open0(r.z, r.w), tab);  // as cust_ztau's alive dropout time
   ez[i] = eta_normal(k0, k1, (uint32_t)i, sweep, tab);
   const SlotPhilox ph(k0, k1, (uint32_t)i, sweep);
+#if CLV_MH_PACK
+  for (int q = 0; 4 * q < S; ++q) {  // the words of mh_chunk_variates (csrc/philox.h), uniforms exposed
+    uint32_t W[12];
+    for (int k = 0; k < 3; ++k) {
+      const u32x4 r = ph(SLOT_MH0 + 3u * (uint32_t)q + (uint32_t)k);
+      W[4 * k] = r.x;
+      W[4 * k + 1] = r.y;
+      W[4 * k + 2] = r.z;
+      W[4 * k + 3] = r.w;
+    }
+    for (int st = 0; st < 4 && 4 * q + st < S; ++st) {
+      const int64_t j = 4 * q + st;
+      const uint32_t a = W[3 * st], b = W[3 * st + 1], c = W[3 * st + 2];
+      tl[j * n + i] = t3_f32(uf24(a), angle12(a, (c >> 24) & 0xfu));
+      tm[j * n + i] = t3_f32(uf24(b), angle12(b, c >> 28));
+      ua[j * n + i] = uf24(c);
+    }
+  }
+#else
   for (int j = 0; j < S; ++j) {
     const u32x4 r = ph(SLOT_MH0 + (uint32_t)j);
     tl[(int64_t)j * n + i] = t3_f32(uf32(r.x), angle_hi(r.z));
     tm[(int64_t)j * n + i] = t3_f32(uf32(r.y), angle_lo(r.z));
     ua[(int64_t)j * n + i] = uf32(r.w);
   }
+#endif
 }
 
 // in: [V 81][cholV 81][A0B0 27][S0B 9] prior block, then xty(K*D) yty(D*D) iwn(3) chi2(3) z(D*K)

@@ -91,9 +91,37 @@ def angle_lo(w):
     return ((w << np.uint32(16)).astype(np.uint32).astype(np.float32) * np.float32(2.0 ** -32)).astype(np.float32)
 
 
+MH_PACK = False  # csrc/philox.h CLV_MH_PACK: four MH steps from three Philox blocks
+
+
+def uf24(w):
+    """(w[23:0] + 1) 2^-24 in (0, 1] (csrc/philox.h uf24; exact in fp32)."""
+    return ((w & np.uint32(0xFFFFFF)).astype(np.float32) * np.float32(2.0 ** -24) + np.float32(2.0 ** -24)).astype(np.float32)
+
+
+def angle12(hi8_word, lo4):
+    """(hi8_word[31:24] . lo4) 2^-12 revolutions (csrc/philox.h angle12; exact in fp32)."""
+    return ((hi8_word >> np.uint32(24)).astype(np.float32) * np.float32(2.0 ** -8)
+            + lo4.astype(np.float32) * np.float32(2.0 ** -12)).astype(np.float32)
+
+
+def mh_step_words(seed, chain, cust, sweep, j):
+    """Uniforms of MH step j: (radius u of t_l, radius u of t_m, angle of t_l, angle of t_m, accept u)."""
+    if MH_PACK:  # chunk q = j // 4: blocks SLOT_MH0 + 3q + {0, 1, 2}; step i = j % 4 takes words 3i..3i+2
+        q, i = divmod(j, 4)
+        W = np.concatenate([customer_blocks(seed, chain, cust, sweep, SLOT_MH0 + 3 * q + k) for k in range(3)], axis=1)
+        a, b, c = W[:, 3 * i], W[:, 3 * i + 1], W[:, 3 * i + 2]
+        return (uf24(a), uf24(b), angle12(a, (c >> np.uint32(24)) & np.uint32(0xF)), angle12(b, c >> np.uint32(28)),
+                uf24(c))
+    w = customer_blocks(seed, chain, cust, sweep, SLOT_MH0 + j)
+    return uf32(w[:, 0]), uf32(w[:, 1]), angle_hi(w[:, 2]), angle_lo(w[:, 2]), uf32(w[:, 3])
+
+
 def sweep_variates(seed, chain, sweep, n, n_steps):
     """The Philox-mode variates of one sweep for customers 0..n-1 (see csrc/philox.h): MH step j
-    uses block SLOT_MH0 + j = (radius of t_l, radius of t_m, two 16-bit angles, accept uniform)."""
+    takes its radius uniforms of t_l / t_m, two angles and the accept uniform from the customer's
+    Philox blocks SLOT_MH0 + ... (MH_PACK: four steps per three blocks, 24-bit uniforms, 12-bit
+    angles; else one block per step, 32-bit words, 16-bit angles)."""
     cust = np.arange(n)
     r = customer_blocks(seed, chain, cust, sweep, SLOT_ZTAU)
     out = dict(u_z=u53(r[:, 0], r[:, 1]), u_tau=u53(r[:, 2], r[:, 3]),
@@ -104,10 +132,10 @@ def sweep_variates(seed, chain, sweep, n, n_steps):
     tm = np.empty((n_steps, n), np.float32)
     ua = np.empty((n_steps, n), np.float32)
     for j in range(n_steps):
-        w = customer_blocks(seed, chain, cust, sweep, SLOT_MH0 + j)
-        tl[j] = t3_f32(uf32(w[:, 0]), angle_hi(w[:, 2]))
-        tm[j] = t3_f32(uf32(w[:, 1]), angle_lo(w[:, 2]))
-        ua[j] = uf32(w[:, 3])
+        ul, um, al, am, uacc = mh_step_words(seed, chain, cust, sweep, j)
+        tl[j] = t3_f32(ul, al)
+        tm[j] = t3_f32(um, am)
+        ua[j] = uacc
     out.update(t_l=tl, t_m=tm, u_acc=ua)
     return out
 

@@ -74,6 +74,24 @@ def test_seed_resolution():
     assert 0 <= resolve_seed(None) < (1 << 63)
 
 
+def test_persistent_residency_margin():
+    """Verdict r2 #6: the persistent kernels need every workgroup resident, so the grid must leave a
+    margin below the occupancy answer (which can be one block per CU high near an SGPR edge).  At
+    2 blocks per CU on 256 CUs (512 slots): c2 / c3 (4 chains x (93 + 1) = 376) and c2 per rank at
+    8 ranks stay persistent; c4 at 8 ranks (a shard of the 1M-customer plan: 496 blocks + 1 level-2
+    workgroup = 497) does not — it runs the fused exchange."""
+    from mcmc_clv_model_amd import _lib
+    from mcmc_clv_model_amd.distributed import plan
+    L = _lib.lib()
+    fits = lambda wgs: bool(L.clv_debug_persist_fits(wgs, 2, 256))  # noqa: E731
+    assert fits(4 * (93 + 1))
+    p8 = plan(1_000_000, 8)
+    nb_rank = -(-(p8.shard(0)[1] - p8.shard(0)[0]) // 256)
+    assert nb_rank == 496 and not fits(nb_rank + 1)
+    assert fits(486) and not fits(487) and not fits(512) and not fits(0)
+    assert not L.clv_debug_persist_fits(10, 0, 256)
+
+
 def test_no_cpu_fallback_without_gpu():
     """The product path raises instead of silently running on the CPU."""
     from mcmc_clv_model_amd import _lib, mcmc_draw_parameters
