@@ -146,9 +146,11 @@ int clv_partials(clv_sampler* s, double** device_ptr, int64_t* n_doubles, int32_
 int clv_copy_partials(clv_sampler* s, void* dst_device_ptr);
 int clv_synchronize(clv_sampler* s);
 int64_t clv_sweeps_done(const clv_sampler* s);
-/* How clv_run launches: out[4] = (persistent 0/1, persistent-kernel workgroups per CU, CUs,
- * workgroups per sweep).  Persistent = one launch for all of a clv_run's sweeps, chosen at create
- * when world_size == 1, Philox mode, every workgroup fits at once, and CLV_PERSISTENT != "0". */
+/* How clv_run launches: out[5] = (persistent 0/1, persistent-kernel workgroups per CU, CUs,
+ * workgroups per sweep, MH-variate chunks each consumer workgroup takes from producer workgroups
+ * (0: no producer / consumer split; CLV_PC_CHUNKS)).  Persistent = one launch for all of a
+ * clv_run's sweeps, chosen at create when world_size == 1, Philox mode, every workgroup fits at
+ * once (with a residency margin), and CLV_PERSISTENT != "0". */
 int clv_launch_info(const clv_sampler* s, int64_t* out);
 /* Sharded runs without a host collective per sweep (world_size > 1, Philox mode): the persistent
  * kernel's level-2 workgroup of each chain writes this rank's unit partials of sweep s straight into

@@ -71,6 +71,8 @@ SweepArgs sweep_args(clv_sampler* s, int init, int fuse = 0) {
   a.mail = s->d_mail;
   a.peers = s->d_peers;
   a.wg_map = s->d_wgmap;
+  a.pc_desc = s->d_pcdesc;
+  a.vbuf = s->d_vbuf;
   a.rank = s->cfg.rank;
   a.lam_out = s->d_lam_alt ? s->d_lam_alt : s->d_lam;
   a.mu_out = s->d_mu_alt ? s->d_mu_alt : s->d_mu;
@@ -310,6 +312,44 @@ std::vector<int32_t> persist_wg_map(int C, int nb, int n_cu) {
   for (int i = 0; i < n_cu - P; ++i) map[P + i] = sorted_single[i];
   return map;
 }
+
+// MH-variate producers / consumers over the placement map above (kernels.hip pc_produce /
+// pc_consume): the customer workgroups of shared CUs (linear [C, P) and n_cu + [C, P), where
+// P = T - n_cu) are consumers that leave their first n_off chunks of drawn-ahead MH variates to
+// the customer workgroups alone on their CUs (linear [P, n_cu) and the level-2 workgroups'
+// partners n_cu + [0, C)), which draw them; tasks are dealt round robin, at most PC_DESC - 2 per
+// producer.  Per-SIMD issue work per sweep at c2 (in units of one wavefront's sweep, v = the
+// variates' share 0.39, 5 chunks): shared 2 (1 - v n_off / 5), alone 1 + 1.66 v n_off / 5 — balanced
+// near n_off = 3 (1.53 and 1.39, from 2 and 1).  Empty if the map is not the paired placement.
+std::vector<int32_t> pc_plan(const std::vector<int32_t>& map, int C, int nb, int n_cu, int n_off) {
+  const int T = (int)map.size();
+  const int P = T - n_cu;
+  std::vector<int32_t> desc;
+  if (n_off <= 0 || P <= C || T > 2 * n_cu || T != C * (nb + 1)) return desc;
+  for (int c = 0; c < C; ++c)  // the paired placement: level-2 workgroups first (persist_wg_map)
+    if (map[c] != ((c << 16) | nb)) return desc;
+  std::vector<int> cons, prod;
+  for (int i = C; i < P; ++i) cons.push_back(i);
+  for (int i = n_cu + C; i < n_cu + P; ++i) cons.push_back(i);
+  for (int i = P; i < n_cu; ++i) prod.push_back(i);
+  for (int i = n_cu; i < n_cu + C; ++i) prod.push_back(i);
+  for (int i : prod)
+    if ((map[i] & 0xFFFF) == nb) return desc;  // (a level-2 workgroup is never a producer)
+  const int per = PC_DESC - 2;
+  while (n_off > 0 && (int64_t)cons.size() * n_off > (int64_t)prod.size() * per) --n_off;
+  if (n_off <= 0 || prod.empty()) return desc;
+  desc.assign((size_t)T * PC_DESC, 0);
+  int t = 0;
+  for (int i : cons) {
+    desc[(size_t)i * PC_DESC] = n_off;
+    for (int q = 0; q < n_off; ++q, ++t) {
+      const int p = prod[t % prod.size()];
+      int32_t* d = &desc[(size_t)p * PC_DESC];
+      d[2 + d[1]++] = (i << 4) | q;
+    }
+  }
+  return desc;
+}
 }  // namespace
 
 extern "C" {
@@ -503,6 +543,21 @@ int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* pri
       std::vector<int32_t> map = persist_wg_map((int)C, (int)nb_local, s->n_cu);
       CLV_HIPC(dalloc(&s->d_wgmap, map.size()));
       CLV_HIPC(hipMemcpy(s->d_wgmap, map.data(), sizeof(int32_t) * map.size(), hipMemcpyHostToDevice));
+      // world size 1: producer / consumer split of the drawn-ahead MH variates (CLV_PC_CHUNKS:
+      // chunks per consumer, 0 = off); full 4-step chunks of drawn-ahead variates only
+      env = std::getenv("CLV_PC_CHUNKS");
+      const int n_off = std::min({env ? std::atoi(env) : 3, g.S / MH_CHUNK_STEPS, PC_CHUNKS});
+      if (s->persistent && s->pre_variates && g.S <= PC_CHUNKS * MH_CHUNK_STEPS && n_off > 0) {
+        const std::vector<int32_t> desc = pc_plan(map, (int)C, (int)nb_local, s->n_cu, n_off);
+        if (!desc.empty()) {
+          CLV_HIPC(dalloc(&s->d_pcdesc, desc.size()));
+          CLV_HIPC(hipMemcpy(s->d_pcdesc, desc.data(), sizeof(int32_t) * desc.size(), hipMemcpyHostToDevice));
+          s->n_vbuf = 2LL * (int64_t)map.size() * PC_CHUNKS * PC_WORDS * BLOCK;
+          CLV_HIPC(dalloc(&s->d_vbuf, (size_t)s->n_vbuf));
+          CLV_HIPC(hipMemset(s->d_vbuf, 0xFF, sizeof(double) * (size_t)s->n_vbuf));  // every slot empty
+          s->pc_chunks = desc[(size_t)C * PC_DESC];
+        }
+      }
     }
   }
 #ifdef CLV_STAMPS
@@ -618,6 +673,8 @@ void clv_destroy(clv_sampler* s) {
   if (s->d_mail) (void)hipFree(s->d_mail);
   if (s->d_peers) (void)hipFree(s->d_peers);
   if (s->d_wgmap) (void)hipFree(s->d_wgmap);
+  if (s->d_pcdesc) (void)hipFree(s->d_pcdesc);
+  if (s->d_vbuf) (void)hipFree(s->d_vbuf);
   if (s->own_stream && s->own) (void)hipStreamDestroy(s->own);
   delete s;
 }
@@ -708,6 +765,7 @@ int clv_launch_info(const clv_sampler* s, int64_t* out) {
   out[1] = s->persist_bpc;
   out[2] = s->n_cu;
   out[3] = (int64_t)(s->g.nb_local + (s->persistent ? 1 : 0)) * s->g.n_chains;
+  out[4] = s->pc_chunks;
   return CLV_OK;
 }
 
@@ -822,6 +880,7 @@ int clv::persist_launch(clv_sampler* s, int64_t n_sweeps) {
     // every hand-off slot empty (all-ones bytes: the sentinel NaN)
     CLV_HIP(hipMemsetAsync(s->d_hyp2, 0xFF, sizeof(double) * 2 * g.n_chains * HS, s->stream));
     CLV_HIP(hipMemsetAsync(s->d_pblock, 0xFF, sizeof(double) * g.n_chains * g.nb_local * g.stride, s->stream));
+    if (s->d_vbuf) CLV_HIP(hipMemsetAsync(s->d_vbuf, 0xFF, sizeof(double) * (size_t)s->n_vbuf, s->stream));
     s->slots_dirty = false;
   }
   const size_t sums_bytes = sizeof(double) * (size_t)g.n_chains * CLV_N_SUM_STATS * g.n;

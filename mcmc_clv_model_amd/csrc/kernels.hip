@@ -1278,12 +1278,13 @@ __device__ __forceinline__ int opaque_uniform(int x) {
   return x;
 }
 
-__device__ __forceinline__ void mh_pre_variates(const SlotPhilox& ph, int S_, const PreVariates& v) {
+// q_first: chunks below it come from producer workgroups (pc_consume) and are not drawn here.
+__device__ __forceinline__ void mh_pre_variates(const SlotPhilox& ph, int S_, const PreVariates& v, int q_first = 0) {
   constexpr int MC = MH_CHUNK_STEPS;
   const int S = opaque_uniform(S_);
 #pragma unroll
   for (int q = 0; q < PRE_STEPS / MC; ++q) {
-    if (q * MC < S) {  // wave-uniform
+    if (q >= q_first && q * MC < S) {  // wave-uniform
       float tl[MC], tm[MC], lu[MC];
       mh_chunk_variates(ph, (uint32_t)q, tl, tm, lu);
       if (q * MC + MC <= S) {  // full chunk
@@ -2101,6 +2102,75 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
   return;
 }
 
+// ---- MH-variate producers and consumers (persistent kernel, world size 1; capi.hip pc_plan) ----
+// c2 runs 1,473 customer wavefronts on 1,024 SIMDs: the SIMDs of the CUs that hold two workgroups
+// run two wavefronts and set the sweep period, the others idle part of it.  The drawn-ahead MH
+// variates of the next sweep are independent of the state, so consumer workgroups (on shared CUs)
+// leave their first chunks to producer workgroups (alone on their CUs), which draw them for the
+// consumer's customers (same Philox counters: same values, same results bit for bit) in their
+// hand-off window and store them as packed float pairs into vbuf; the consumer reads them at the
+// start of that sweep.  A word is its own arrival flag (the all-ones pattern is never a pair of
+// finite floats): the consumer polls until its words are there, copies them to its LDS pool and
+// empties the slots.  Slot reuse (sweep s + 2) follows the level-2 hand-off: a producer writes
+// them only after (beta, Sigma) of s + 1, published after the consumer's partial of s, which
+// leaves after its resets (write-through stores, waited for before the partial).
+__device__ __forceinline__ double pack_f2(float lo, float hi) {
+  return bitsd((uint64_t)__float_as_uint(lo) | ((uint64_t)__float_as_uint(hi) << 32));
+}
+__device__ __forceinline__ float lo_f(double w) { return __uint_as_float((uint32_t)dbits(w)); }
+__device__ __forceinline__ float hi_f(double w) { return __uint_as_float((uint32_t)(dbits(w) >> 32)); }
+
+__device__ __forceinline__ double* pc_slot(const SweepArgs& a, int64_t s, int T, int L, int q) {
+  return a.vbuf + (((int64_t)(s & 1) * T + L) * PC_CHUNKS + q) * PC_WORDS * BLOCK;
+}
+
+// Producer: chunk q of the MH variates of sweep s for consumer workgroup `cons`'s customers.
+__device__ __forceinline__ void pc_produce(const SweepArgs& a, int32_t task, int64_t s, int T, int tid) {
+  const int cons = task >> 4, q = task & 15;
+  const int32_t m = a.wg_map[cons];
+  uint32_t kk0, kk1;
+  chain_key(a.r.seed, (int64_t)a.r.chain_first + (m >> 16), &kk0, &kk1);
+  const uint32_t gi = (uint32_t)(a.g.shard_begin + (int64_t)(m & 0xFFFF) * BLOCK + tid);
+  float tl[MH_CHUNK_STEPS], tm[MH_CHUNK_STEPS], lu[MH_CHUNK_STEPS];
+  mh_chunk_variates(SlotPhilox(kk0, kk1, gi, (uint32_t)s), (uint32_t)q, tl, tm, lu);
+  double* dst = pc_slot(a, s, T, cons, q) + tid;
+#pragma unroll
+  for (int w = 0; w < MH_CHUNK_STEPS; ++w) st_wt(dst + w * BLOCK, pack_f2(tl[w], tm[w]));
+  st_wt(dst + 4 * BLOCK, pack_f2(lu[0], lu[1]));
+  st_wt(dst + 5 * BLOCK, pack_f2(lu[2], lu[3]));
+}
+
+// Consumer: chunks [0, n_off) of this workgroup's MH variates of sweep s into the LDS pool, slots
+// emptied after.  False if a wait timed out (the abort flag is raised: every wave leaves at its
+// next wait).
+__device__ __forceinline__ bool pc_consume(const SweepArgs& a, int n_off, int64_t s, int T, int L, const PreVariates& v) {
+  for (int q = 0; q < n_off; ++q) {
+    double* src = pc_slot(a, s, T, L, q) + v.lane;
+    double w[PC_WORDS];
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (uint32_t poll = 0;; ++poll) {
+      bool ok = true;
+#pragma unroll
+      for (int k = 0; k < PC_WORDS; ++k) {
+        w[k] = ld_wt(src + k * BLOCK);
+        ok = ok & slot_full(w[k]);
+      }
+      if (__all(ok)) break;
+      if (wait_expired(a, t0, poll)) return false;
+      __builtin_amdgcn_s_sleep(1);
+    }
+#pragma unroll
+    for (int k = 0; k < MH_CHUNK_STEPS; ++k) v.t[(q * MH_CHUNK_STEPS + k) * BLOCK + v.lane] = make_float2(lo_f(w[k]), hi_f(w[k]));
+    v.u[(q * MH_CHUNK_STEPS + 0) * BLOCK + v.lane] = lo_f(w[4]);
+    v.u[(q * MH_CHUNK_STEPS + 1) * BLOCK + v.lane] = hi_f(w[4]);
+    v.u[(q * MH_CHUNK_STEPS + 2) * BLOCK + v.lane] = lo_f(w[5]);
+    v.u[(q * MH_CHUNK_STEPS + 3) * BLOCK + v.lane] = hi_f(w[5]);
+#pragma unroll
+    for (int k = 0; k < PC_WORDS; ++k) st_wt(src + k * BLOCK, slot_empty());
+  }
+  return true;
+}
+
 // P2P: world size > 1 with the peer exchange (a separate instance, so that the world-size-1
 // kernel carries none of its registers or LDS).
 template <int D, int K, bool P2P>
@@ -2127,6 +2197,13 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
   const int tid = threadIdx.x;
   const int64_t wgi = (int64_t)c * (g.nb_local + 1) + b;
   const int64_t it_stamp = n_sweeps >= 2 ? n_sweeps - 2 : 0;  // diagnostic build: one sweep's timeline
+  // producer / consumer role of this (dispatch-order) workgroup; none in the P2P instance
+  const int T_wg = gridDim.x * gridDim.y, L_wg = blockIdx.y * gridDim.x + blockIdx.x;
+  int pc_off = 0, pc_ntask = 0;
+  if (!P2P && a.pc_desc) {
+    pc_off = a.pc_desc[L_wg * PC_DESC];
+    pc_ntask = a.pc_desc[L_wg * PC_DESC + 1];
+  }
   (void)wgi;
   (void)it_stamp;
   uint32_t k0, k1;
@@ -2168,6 +2245,8 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
     const bool stp = tid == 0 && it == it_stamp;
     (void)stp;
     CLV_P_STAMP(a.stamps, wgi, 0, stp);
+    // consumer: this sweep's first MH-variate chunks from the producers (drawn during sweep s - 1)
+    if (pc_off > 0 && it > 0 && pre && !pc_consume(a, pc_off, s, T_wg, L_wg, pv)) s_abort = 1;
     if (it > 0) {  // wait for (beta, Sigma) of sweep s (wavefront 0 polls, one slot per lane)
       if (tid < 64) {
         const double* src = hyp_c + (int64_t)(s & 1) * g.n_chains * HS;
@@ -2227,12 +2306,15 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
       cust_store<D, K>(cu, out, a, c, s, stored, false);
       if (it + 1 < n_sweeps) {
         cust_ztau<D, K, false>(cu, a, s + 1, k0, k1, nullptr, exp_tab);
-        if (pre) mh_pre_variates(SlotPhilox(k0, k1, cu.gi, (uint32_t)(s + 1)), g.S, pv);
+        if (pre) mh_pre_variates(SlotPhilox(k0, k1, cu.gi, (uint32_t)(s + 1)), g.S, pv, pc_off);
         if constexpr (D == 3) {
           if (pre) zeta_lds[tid] = eta_normal(k0, k1, cu.gi, s + 1, exp_tab);
         }
       }
     }
+    // producer: consumers' chunks of sweep s + 1 (every lane: the consumer polls all of its lanes)
+    if (pre && it + 1 < n_sweeps)
+      for (int k = 0; k < pc_ntask; ++k) pc_produce(a, a.pc_desc[L_wg * PC_DESC + 2 + k], s + 1, T_wg, tid);
     CLV_P_STAMP(a.stamps, wgi, 6, stp);
   }
   if (cu.active) {  // the carried state, once per launch (adopted by the host if nothing aborted)

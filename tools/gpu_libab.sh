@@ -7,7 +7,7 @@ for W in "$@"; do
   for L in $LIBS; do
     tag=$(echo $L | tr '/' '_')
     if [ "$L" = "default" ]; then unset CLV_LIB_PATH; else export CLV_LIB_PATH=$R/$L; fi
-    timeout -k 10 300 python bench.py --workload $W --no-cpu-baseline --scaling-configs "" --steps ${STEPS:-2000} --warmup 200 \
+    timeout -k 10 300 python bench.py --workload $W --no-cpu-baseline --scaling-configs "" --no-c1-leg --steps ${STEPS:-2000} --warmup 200 \
       --timing-steps 500 > gpurun_out/lab_${W}_${tag}.log 2>&1; rc=$?
     echo ${W} ${L} rc=$rc; python - "gpurun_out/lab_${W}_${tag}.log" <<'PY'
 import json,sys

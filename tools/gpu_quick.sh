@@ -7,7 +7,7 @@ if [ "${TESTS:-0}" = "1" ]; then
   [ $rc -le 1 ] || exit $rc
 fi
 for W in "$@"; do
-  timeout -k 10 300 python bench.py --workload $W --no-cpu-baseline --scaling-configs "" --steps ${STEPS:-3000} --warmup 300 --timing-steps 1000 > gpurun_out/q_$W.log 2>&1; rc=$?
+  timeout -k 10 300 python bench.py --workload $W --no-cpu-baseline --scaling-configs "" --no-c1-leg --steps ${STEPS:-3000} --warmup 300 --timing-steps 1000 > gpurun_out/q_$W.log 2>&1; rc=$?
   echo ${W}_rc=$rc; python - "$W" <<'PY'
 import json,sys
 l=json.loads(open(f"gpurun_out/q_{sys.argv[1]}.log").read().strip().splitlines()[-1])
