@@ -75,21 +75,22 @@ def test_seed_resolution():
 
 
 def test_persistent_residency_margin():
-    """Verdict r2 #6: the persistent kernels need every workgroup resident, so the grid must leave a
-    margin below the occupancy answer (which can be one block per CU high near an SGPR edge).  At
-    2 blocks per CU on 256 CUs (512 slots): c2 / c3 (4 chains x (93 + 1) = 376) and c2 per rank at
-    8 ranks stay persistent; c4 at 8 ranks (a shard of the 1M-customer plan: 496 blocks + 1 level-2
-    workgroup = 497) does not — it runs the fused exchange."""
+    """Verdict r2 #6: the persistent kernels need every workgroup resident, so the grid must fit the
+    admitted blocks per CU — min(occupancy API, 8, floor(800 / (ceil(sgpr/16)*16 + 16))), the
+    MI355X guide's rule, at the maximum SGPR count — less a margin of one slot per 32 CUs.  At
+    2 blocks per CU on 256 CUs (512 slots, 504 allowed): c2 / c3 (4 chains x (93 + 1) = 376) and
+    c4 at 8 ranks (a shard of the 1M-customer plan: 496 blocks + 1 level-2 workgroup = 497) fit."""
     from mcmc_clv_model_amd import _lib
     from mcmc_clv_model_amd.distributed import plan
     L = _lib.lib()
-    fits = lambda wgs: bool(L.clv_debug_persist_fits(wgs, 2, 256))  # noqa: E731
+    fits = lambda wgs, bpc=2: bool(L.clv_debug_persist_fits(wgs, bpc, 256))  # noqa: E731
     assert fits(4 * (93 + 1))
     p8 = plan(1_000_000, 8)
     nb_rank = -(-(p8.shard(0)[1] - p8.shard(0)[0]) // 256)
-    assert nb_rank == 496 and not fits(nb_rank + 1)
-    assert fits(486) and not fits(487) and not fits(512) and not fits(0)
+    assert nb_rank == 496 and fits(nb_rank + 1)
+    assert fits(504) and not fits(505) and not fits(512) and not fits(0)
     assert not L.clv_debug_persist_fits(10, 0, 256)
+    assert fits(6 * 256 - 8, 7) and not fits(6 * 256 - 7, 7)  # the SGPR term caps 7 / 8 blocks per CU at 6
 
 
 def test_no_cpu_fallback_without_gpu():
