@@ -1324,6 +1324,16 @@ int clv_debug_hyper_variates(uint64_t seed, int32_t chain, uint32_t sweep, doubl
   return CLV_OK;
 }
 
+int clv_debug_pc_plan(int32_t n_chains, int32_t nb, int32_t n_cu, int32_t n_off, int32_t* out) {
+  if (!out || n_chains < 1 || nb < 0 || n_cu < 1 || n_chains >= (1 << 15) || nb >= (1 << 16))
+    return fail(CLV_EINVAL, "bad arguments");
+  const std::vector<int32_t> d = pc_plan(persist_wg_map(n_chains, nb, n_cu), n_chains, nb, n_cu, n_off);
+  const size_t T = (size_t)n_chains * (nb + 1);
+  if (d.empty()) std::fill(out, out + T * PC_DESC, 0);
+  else std::copy(d.begin(), d.end(), out);
+  return CLV_OK;
+}
+
 int clv_debug_persist_fits(int64_t grid_wgs, int32_t blocks_per_cu, int32_t n_cu) {
   return persist_grid_fits(grid_wgs, blocks_per_cu, n_cu) ? 1 : 0;
 }

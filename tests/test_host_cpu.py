@@ -93,6 +93,41 @@ def test_persistent_residency_margin():
     assert fits(6 * 256 - 8, 7) and not fits(6 * 256 - 7, 7)  # the SGPR term caps 7 / 8 blocks per CU at 6
 
 
+@pytest.mark.parametrize("C,nb,n_off", [(4, 93, 3), (3, 93, 3), (4, 93, 5), (2, 200, 2), (8, 40, 1), (4, 10, 3)])
+def test_producer_consumer_plan(C, nb, n_off):
+    """The persistent grid's MH-variate producer / consumer roles (capi.hip pc_plan): consumers are the
+    customer workgroups of shared CUs (linear [C, P) and 256 + [C, P), P = T - 256), producers the
+    customer workgroups alone on their CUs; every consumer chunk is drawn by exactly one producer,
+    no producer has more than 6 tasks, level-2 workgroups take no part, and with no shared CUs
+    (c1-size grids) there is no split."""
+    import ctypes
+    import numpy as np
+    from mcmc_clv_model_amd import _lib
+    L = _lib.lib()
+    n_cu = 256
+    T = C * (nb + 1)
+    out = np.zeros((T, 8), np.int32)
+    wmap = np.zeros(T, np.int32)
+    assert L.clv_debug_pc_plan(C, nb, n_cu, n_off, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))) == 0
+    assert L.clv_debug_wg_map(C, nb, n_cu, wmap.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))) == 0
+    P = T - n_cu
+    if P <= C:
+        assert not out.any()
+        return
+    cons = set(range(C, P)) | set(range(n_cu + C, n_cu + P))
+    k = int(out[C, 0])
+    assert 1 <= k <= n_off
+    assert all(out[i, 0] == (k if i in cons else 0) for i in range(T))
+    tasks = []
+    for i in range(T):
+        nt = int(out[i, 1])
+        assert nt <= 6 and (nt == 0 or i not in cons)
+        assert nt == 0 or (wmap[i] & 0xFFFF) != nb  # never a level-2 workgroup
+        tasks += [int(v) for v in out[i, 2:2 + nt]]
+    assert sorted(tasks) == sorted((i << 4) | q for i in cons for q in range(k))
+    assert all((wmap[i] & 0xFFFF) != nb for i in cons)
+
+
 def test_no_cpu_fallback_without_gpu():
     """The product path raises instead of silently running on the CPU."""
     from mcmc_clv_model_amd import _lib, mcmc_draw_parameters
