@@ -146,11 +146,14 @@ int clv_partials(clv_sampler* s, double** device_ptr, int64_t* n_doubles, int32_
 int clv_copy_partials(clv_sampler* s, void* dst_device_ptr);
 int clv_synchronize(clv_sampler* s);
 int64_t clv_sweeps_done(const clv_sampler* s);
-/* How clv_run launches: out[5] = (persistent 0/1, persistent-kernel workgroups per CU, CUs,
+/* How clv_run launches: out[6] = (persistent 0/1, persistent-kernel workgroups per CU, CUs,
  * workgroups per sweep, MH-variate chunks each consumer workgroup takes from producer workgroups
- * (0: no producer / consumer split; CLV_PC_CHUNKS)).  Persistent = one launch for all of a
- * clv_run's sweeps, chosen at create when world_size == 1, Philox mode, every workgroup fits at
- * once (with a residency margin), and CLV_PERSISTENT != "0". */
+ * (0: no producer / consumer split; CLV_PC_CHUNKS), stride-kernel workgroups (0: none)).
+ * Persistent = one launch for all of a clv_run's sweeps with every customer block resident, chosen
+ * at create when world_size == 1, Philox mode, every workgroup fits at once (with a residency
+ * margin), and CLV_PERSISTENT != "0".  Otherwise at world size 1 in Philox mode the stride kernel
+ * (CLV_STRIDE != "0"): one launch for all sweeps too, a resident grid taking (sweep, chain, block)
+ * tasks in order with the state in HBM; else one launch per sweep. */
 int clv_launch_info(const clv_sampler* s, int64_t* out);
 /* Sharded runs without a host collective per sweep (world_size > 1, Philox mode): the persistent
  * kernel's level-2 workgroup of each chain writes this rank's unit partials of sweep s straight into

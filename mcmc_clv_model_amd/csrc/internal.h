@@ -95,6 +95,9 @@ struct clv_sampler {
                                     // launch leaves them empty; only an aborted one does not)
   int64_t last_persist_n = 0;       // sweeps of the last persistent launch (rollback), 0 = none
   bool persistent = false;          // clv_run uses persist_kernel (all workgroups resident)
+  int stride_grid = 0;              // > 0: clv_run uses stride_kernel on this many resident workgroups
+  uint32_t* d_ticket = nullptr;     // stride kernel: the launch's ticket counter
+  uint32_t* d_done = nullptr;       // stride kernel: [chain][block] sweeps of the launch whose state is final
   int persist_bpc = 0, n_cu = 0;    // persist_kernel occupancy (workgroups per CU), CUs
   // world size > 1: persistent kernel with the peer (xGMI) exchange
   bool p2p_capable = false;         // the grid fits at once and the unit partials fit UMAIL

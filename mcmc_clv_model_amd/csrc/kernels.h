@@ -9,6 +9,7 @@ namespace clv {
 
 constexpr int BLOCK = CLV_BLOCK;       // customers (lanes) per sweep workgroup
 constexpr int HS = 64;                 // doubles of hyper state per chain
+constexpr int H_TAG = 63;              // stride kernel: the sweep a published (beta, Sigma) belongs to
 constexpr int TAPE_HYPER = 40;         // doubles of hyper variates per recorded sweep
 constexpr int MAX_WORLD = 64;             // peer exchange: ranks (mail pointers staged in LDS)
 constexpr int UMAIL = 2048;            // persistent kernel, world size > 1: LDS doubles for this rank's
@@ -121,6 +122,11 @@ struct SweepArgs {
   // vbuf: [2 (sweep parity)][linear workgroup][PRE_CHUNKS][PC_WORDS][BLOCK] packed float pairs.
   const int32_t* pc_desc;
   double* vbuf;
+  // stride kernel (world size 1, grids too large to be resident): ticket counter of the launch's
+  // (sweep, chain, block) tasks and, per (chain, block), the number of this launch's sweeps whose
+  // state is final (both zeroed by the host before each launch)
+  uint32_t* ticket;
+  uint32_t* done;
   // persistent kernel: the carried state at the end of a launch goes to these (the host swaps them
   // with lam / mu / hyper only if no wave aborted), the bound on every wait (s_memrealtime ticks,
   // 100 MHz) and a host-mapped copy of ctrl->abort (read by the host after the launch, no D2H copy)
@@ -147,6 +153,9 @@ hipError_t launch_group(const GroupArgs& a, hipStream_t st);
 hipError_t launch_persist(const SweepArgs& a, int64_t s_first, int64_t n_sweeps, hipStream_t st,
                           hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 hipError_t persist_occupancy(int D, int K, bool p2p, int* blocks_per_cu);
+hipError_t launch_stride(const SweepArgs& a, int64_t s_first, int64_t n_sweeps, int grid, hipStream_t st,
+                         hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
+hipError_t stride_occupancy(int D, int K, int* blocks_per_cu);
 hipError_t launch_hyper(const HyperArgs& a, bool replay, hipStream_t st);
 hipError_t launch_set_hyper(int D, int K, int n_chains, double* hyper, const double* beta_sigma,
                             double omega2, hipStream_t st);

@@ -1035,7 +1035,9 @@ struct Cust {
 
 // Phase A1: the customer's loads (CBS row, covariates, state), issued before the workgroup's
 // exp-table barrier so their latency overlaps it.
-template <int D, int K, bool CL>
+// WT: the state (lambda, mu) with write-through-coherent loads (the stride kernel: another
+// workgroup, possibly on another XCD, stored it during this launch).
+template <int D, int K, bool CL, bool WT = false>
 __device__ __forceinline__ void cust_load(Cust<D, K, CL>& u, const SweepArgs& a, int c) {
   const Geometry& g = a.g;
   const int64_t i = u.i;
@@ -1050,8 +1052,13 @@ __device__ __forceinline__ void cust_load(Cust<D, K, CL>& u, const SweepArgs& a,
     for (int k = 1; k < K; ++k) u.xr_[k] = a.cov[(int64_t)(k - 1) * g.n + i];
   }
   const int64_t ci = (int64_t)c * g.n + i;
-  u.lam = a.lam[ci];
-  u.mu = a.mu[ci];
+  if constexpr (WT) {
+    u.lam = ld_wt(a.lam + ci);
+    u.mu = ld_wt(a.mu + ci);
+  } else {
+    u.lam = a.lam[ci];
+    u.mu = a.mu[ci];
+  }
   u.xi = a.x[i];
   u.gi = (uint32_t)(g.shard_begin + i);
 }
@@ -1221,25 +1228,26 @@ __device__ __forceinline__ void mh_step(Cust<D, K, CL>& u, double s00, double s1
 // the next chunk's variates form one branch-free basic block, so the scheduler can interleave
 // that work with the dependent fp64 accept/reject chain.  The last chunk's steps beyond S are
 // padded with log U = +inf (never accepted: the state is unchanged) instead of a branch.
-template <int D, int K, bool CL>
+// q0: the first chunk run here (the chunks below it were run from drawn-ahead variates).
+template <bool PIPE = (SWEEP_MH_PIPELINE != 0), int D, int K, bool CL>
 __device__ __forceinline__ void mh_run(Cust<D, K, CL>& cu, const SlotPhilox& ph, double s00, double s11, int S,
-                                       const double* exp_tab) {
+                                       const double* exp_tab, int q0 = 0) {
   constexpr int MC = MH_CHUNK_STEPS;
   const int n_chunks = (S + MC - 1) / MC;
-  if (n_chunks <= 0) return;
+  if (n_chunks <= q0) return;
   float tl[MC], tm[MC], lu[MC];
-#if SWEEP_MH_PIPELINE == 0
+  if constexpr (!PIPE) {
   // no software pipeline (occupancy hides the latency instead): variates, then the chunk's steps
-  for (int ch = 0; ch < n_chunks; ++ch) {
+  for (int ch = q0; ch < n_chunks; ++ch) {
     mh_chunk_variates(ph, (uint32_t)ch, tl, tm, lu);
     const int rem = S - ch * MC;
 #pragma unroll
     for (int st = 0; st < MC; ++st) mh_step(cu, s00, s11, tl[st], tm[st], st < rem ? lu[st] : __builtin_inff(), exp_tab);
   }
   return;
-#endif
-  mh_chunk_variates(ph, 0u, tl, tm, lu);
-  for (int ch = 0; ch + 1 < n_chunks; ++ch) {
+  }
+  mh_chunk_variates(ph, (uint32_t)q0, tl, tm, lu);
+  for (int ch = q0; ch + 1 < n_chunks; ++ch) {
     float ntl[MC], ntm[MC], nlu[MC];
     mh_chunk_variates(ph, (uint32_t)(ch + 1), ntl, ntm, nlu);
 #pragma unroll
@@ -1279,11 +1287,12 @@ __device__ __forceinline__ int opaque_uniform(int x) {
 }
 
 // q_first: chunks below it come from producer workgroups (pc_consume) and are not drawn here.
+template <int NQ = PRE_STEPS / MH_CHUNK_STEPS>
 __device__ __forceinline__ void mh_pre_variates(const SlotPhilox& ph, int S_, const PreVariates& v, int q_first = 0) {
   constexpr int MC = MH_CHUNK_STEPS;
   const int S = opaque_uniform(S_);
 #pragma unroll
-  for (int q = 0; q < PRE_STEPS / MC; ++q) {
+  for (int q = 0; q < NQ; ++q) {
     if (q >= q_first && q * MC < S) {  // wave-uniform
       float tl[MC], tm[MC], lu[MC];
       mh_chunk_variates(ph, (uint32_t)q, tl, tm, lu);
@@ -1306,13 +1315,13 @@ __device__ __forceinline__ void mh_pre_variates(const SlotPhilox& ph, int S_, co
   }
 }
 
-template <int D, int K, bool CL>
+template <int NQ = PRE_STEPS / MH_CHUNK_STEPS, int D, int K, bool CL>
 __device__ __forceinline__ void mh_run_pre(Cust<D, K, CL>& cu, const PreVariates& v, double s00, double s11, int S,
                                            const double* exp_tab) {
   constexpr int MC = MH_CHUNK_STEPS;
   S = opaque_uniform(S);
 #pragma unroll
-  for (int q = 0; q < PRE_STEPS / MC; ++q) {
+  for (int q = 0; q < NQ; ++q) {
     if (q * MC < S) {  // wave-uniform
       float2 t[MC];
       float u[MC];
@@ -1417,7 +1426,9 @@ __device__ __forceinline__ CustOut<D> cust_finish(Cust<D, K, CL>& u, const Sweep
 
 // Phase C2: storage (bi:402-412, tri:539-571) — issued after the workgroup's partial has been
 // handed off, so the hand-off's store drain does not wait for them — and the carried state.
-template <int D, int K, bool CL>
+// WT: state and running sums with write-through stores (and coherent loads of the sums): the
+// stride kernel's next sweep of this block may run on another XCD.
+template <int D, int K, bool CL, bool WT = false>
 __device__ __forceinline__ void cust_store(const Cust<D, K, CL>& u, const CustOut<D>& o, const SweepArgs& a, int c,
                                            int64_t s, bool stored, bool store_state) {
   const Geometry& g = a.g;
@@ -1434,27 +1445,36 @@ __device__ __forceinline__ void cust_store(const Cust<D, K, CL>& u, const CustOu
     }
     if (a.sums) {
       double* sm = a.sums + (int64_t)c * CLV_N_SUM_STATS * g.n + i;
-      sm[CLV_SUM_LAMBDA * g.n] += o.lam;
-      sm[CLV_SUM_MU * g.n] += o.mu;
-      sm[CLV_SUM_Z * g.n] += u.z ? 1.0 : 0.0;
-      sm[CLV_SUM_LOG_LAMBDA * g.n] += o.lgl;
-      sm[CLV_SUM_LOG_MU * g.n] += o.lgm;
-      sm[CLV_SUM_LAMBDA2 * g.n] += o.lam * o.lam;
-      sm[CLV_SUM_MU2 * g.n] += o.mu * o.mu;
+      auto acc = [&](int k, double v) {
+        if constexpr (WT) st_wt(sm + k * g.n, ld_wt(sm + k * g.n) + v);
+        else sm[k * g.n] += v;
+      };
+      acc(CLV_SUM_LAMBDA, o.lam);
+      acc(CLV_SUM_MU, o.mu);
+      acc(CLV_SUM_Z, u.z ? 1.0 : 0.0);
+      acc(CLV_SUM_LOG_LAMBDA, o.lgl);
+      acc(CLV_SUM_LOG_MU, o.lgm);
+      acc(CLV_SUM_LAMBDA2, o.lam * o.lam);
+      acc(CLV_SUM_MU2, o.mu * o.mu);
       if constexpr (D == 3) {
-        sm[CLV_SUM_ETA * g.n] += o.eta;
-        sm[CLV_SUM_LOG_ETA * g.n] += o.leta;
+        acc(CLV_SUM_ETA, o.eta);
+        acc(CLV_SUM_LOG_ETA, o.leta);
       }
-      sm[CLV_SUM_MU_CAPPED * g.n] += fmin(o.mu, CLV_SUMMARY_MU_CAP);  // np.clip(mu, None, 0.05)
-      sm[CLV_SUM_TAU * g.n] += u.tau;
+      acc(CLV_SUM_MU_CAPPED, fmin(o.mu, CLV_SUMMARY_MU_CAP));  // np.clip(mu, None, 0.05)
+      acc(CLV_SUM_TAU, u.tau);
     }
     if (a.qstore)  // one coalesced 8-byte store per lane
       a.qstore[((int64_t)c * g.n_draws + dr) * g.n + i] = make_float2((float)o.lam, (float)o.mu);
   }
   if (store_state) {
     const int64_t ci = (int64_t)c * g.n + i;
-    a.lam[ci] = o.lam;
-    a.mu[ci] = o.mu;
+    if constexpr (WT) {
+      st_wt(a.lam + ci, o.lam);
+      st_wt(a.mu + ci, o.mu);
+    } else {
+      a.lam[ci] = o.lam;
+      a.mu[ci] = o.mu;
+    }
   }
 }
 
@@ -2324,6 +2344,317 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Stride kernel (world size 1, Philox mode, grids too large to be resident at once: c4, c5).
+// One launch runs n_sweeps sweeps on a resident grid of G workgroups that take (sweep, chain,
+// block) tasks from a ticket counter in order, one at a time, with the state in HBM:
+//   wait until the block's previous sweep is final (its `done` count) -> loads, z / tau (state
+//   only) -> [the chain's (beta, Sigma) of this sweep not published yet: draw the first MH
+//   variate chunks ahead into LDS, then wait] -> MH, finish, the block partial (write-through),
+//   state / draws / running sums (write-through) -> `done` -> the fused path's two-level arrival:
+//   the unit's last block sums the unit, the chain's last unit reduces every unit partial in the
+//   fixed order and draws (beta, Sigma) of the next sweep, published into a sweep-parity slot set
+//   with the sweep as a tag (hyp2[.][H_TAG]), the next draw's variates come from the chain's last
+//   block (hvar, by sweep parity).
+// So the level-2 draw of sweep s no longer idles the GPU: the other workgroups already load and
+// prepare their first task of sweep s + 1, and there are no kernel boundaries between sweeps.
+// Sums are formed exactly as in the fused path (same partials, same orders): results are bitwise
+// those of the launch-per-sweep kernel.  Progress: a workgroup holds one task at a time and the
+// holder of the oldest unfinished task waits only on older sweeps, so with every workgroup
+// resident nothing waits forever; every wait is bounded anyway (wait_ticks), a timed-out wave
+// raises ctrl->abort and the host restores the state the launch started from.  Counters are
+// monotonic within a launch (the unit's last block of sweep it sees (it + 1) * blocks - 1).
+// ---------------------------------------------------------------------------------------------
+#ifndef CLV_STRIDE_PRE
+#define CLV_STRIDE_PRE(D) ((D) == 2 ? 2 : 0)
+#endif
+#ifndef CLV_STRIDE_FRESH_ARGS
+#define CLV_STRIDE_FRESH_ARGS 1
+#endif
+#ifndef CLV_STRIDE_PIPE
+#define CLV_STRIDE_PIPE 0  // (4 waves per SIMD hide the MH chain's latency; the pipeline's registers spilled)
+#endif
+template <int D, int K>
+struct StridePre {  // MH-variate chunks drawn ahead while (beta, Sigma) are awaited (LDS: 12 KiB each)
+  static constexpr int value = CLV_STRIDE_PRE(D);
+};
+
+// The kernel arguments re-read from the kernarg segment through an opaque pointer: in a loop over
+// tasks the compiler otherwise loads every argument once at entry and keeps them all live in SGPRs
+// (hundreds of SGPR spills into VGPR lanes), instead of scalar loads where they are used.
+__device__ __forceinline__ const SweepArgs& kernargs_fresh() {
+  auto p4 = (const __attribute__((address_space(4))) SweepArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p4));
+  return *(const SweepArgs*)p4;
+}
+
+// Lane l of one wavefront: the level-2 draw's Philox variate of record slot l (hyper_variates'
+// layout of the fused path's hvar: [0, 3) inverse-Wishart normals, [3, 6) chi-squares, [8, 8 + DK)
+// beta normals), 0 elsewhere.
+template <int D, int K>
+__device__ __noinline__ double stride_hyper_variate(const SweepArgs& a, uint32_t k0, uint32_t k1, int64_t hs, int l) {
+  if (l < D * (D - 1) / 2) return hyper_normal(k0, k1, HSLOT_NORMAL0 + l, (uint32_t)hs);
+  if (l >= 3 && l < 3 + D) return chi2_draw(k0, k1, (uint32_t)hs, l - 3, a.h.nu_n - D + 1 + (l - 3));
+  if (l >= 8 && l < 8 + D * K) return hyper_normal(k0, k1, HSLOT_BETA_NORMAL0 + (l - 8), (uint32_t)hs);
+  return 0.0;
+}
+
+template <int D, int K>
+__device__ __forceinline__ void stride_body(const SweepArgs& a0, int64_t s_first, int64_t n_sweeps) {
+  const SweepArgs& a = a0;
+  constexpr int NT = BLOCK;
+  constexpr int NXY = K * D;
+  constexpr int NYY = D * (D + 1) / 2;
+  constexpr int NS = NXY + NYY + 1;
+  constexpr bool CL = CovLds<D, K>::value;
+  constexpr int NPRE = StridePre<D, K>::value;
+  constexpr int POOL = NPRE > 0 ? NPRE * MH_CHUNK_STEPS * BLOCK * 12 : 16;
+  __shared__ double red[BLOCK / 64][NS];
+  __shared__ double tot[NS];
+  __shared__ __attribute__((aligned(16))) double exp_tab[D == 3 ? FAST_TAB_N3 : FAST_TAB_N];
+  __shared__ double Hs[HS];
+  __shared__ double cov_s[CL ? (K - 1) * BLOCK : 1];
+  __shared__ __attribute__((aligned(16))) char pool[POOL];
+  __shared__ double var_iw[4], var_chi[4], var_noise[32];
+  __shared__ L2Scratch l2;
+  __shared__ uint32_t s_tk, s_last, s_abort, s_ready;
+  __shared__ int64_t s_hkey;  // it * n_chains + c of the (beta, Sigma) held in Hs, -1 = none
+  const int tid0 = threadIdx.x;
+  fast_tab_fill(exp_tab, tid0, BLOCK, D == 3);
+  stage_prior(a.h.V, &l2);  // any workgroup may draw a chain's level 2
+  if (tid0 == 0) {
+    s_abort = 0;
+    s_hkey = -1;
+  }
+  __syncthreads();
+  for (;;) {
+#if CLV_STRIDE_FRESH_ARGS
+    const SweepArgs& a = kernargs_fresh();
+#endif
+    // per-lane values recomputed every task from an opaque lane index (held across the loop they
+    // were hoisted, kept live and spilled)
+    int tid = tid0;
+    asm volatile("" : "+v"(tid));
+    const int wave = tid >> 6;
+    const Geometry& g = a.g;
+    const int64_t nb = g.nb_local;
+    const int64_t ntask = (int64_t)g.n_chains * nb;  // tasks per sweep
+    const int64_t total = n_sweeps * ntask;
+    const int bpu = g.blocks_per_unit;
+    const int64_t n_units = (nb + bpu - 1) / bpu;  // units of a chain in this launch
+    const PreVariates pv{(float2*)pool, (float*)(pool + NPRE * MH_CHUNK_STEPS * BLOCK * 8), tid};
+    if (tid == 0) s_tk = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const uint32_t k = __builtin_amdgcn_readfirstlane(s_tk);  // (the host keeps total + grid < 2^32)
+    if ((int64_t)k >= total || s_abort) break;
+    const uint32_t it32 = k / (uint32_t)ntask;
+    const uint32_t rr = k - it32 * (uint32_t)ntask;
+    const int c = (int)(rr / (uint32_t)nb);
+    const int b = (int)(rr - (uint32_t)c * (uint32_t)nb);
+    const int64_t it = it32;
+    const int64_t s = uniform64(s_first + it);
+    const int64_t cb = (int64_t)c * nb + b;
+    // (1) this block's state of sweep s - 1 is final (its task of the previous sweep counted it)
+    if (it > 0 && tid < 64) {
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      for (uint32_t poll = 0;; ++poll) {
+        const uint32_t d = __hip_atomic_load(a.done + cb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (d >= (uint32_t)it) break;
+        if (wait_expired(a, t0, poll)) {
+          if (tid == 0) s_abort = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    __syncthreads();
+    if (s_abort) break;
+    // (2) loads, z / tau
+    Cust<D, K, CL> cu;
+    cu.cl = cov_s + tid;
+    {
+      const int64_t i = (int64_t)b * BLOCK + tid;
+      cu.active = i < g.n;
+      cu.i = cu.active ? i : (g.n > 0 ? g.n - 1 : 0);
+    }
+    cust_load<D, K, CL, true>(cu, a, c);
+    uint32_t k0, k1;
+    chain_key(a.r.seed, (int64_t)a.r.chain_first + c, &k0, &k1);
+    if (cu.active) cust_ztau<D, K, false>(cu, a, s, k0, k1, nullptr, exp_tab);
+    // (3) (beta, Sigma) of sweep s for chain c (LDS copy kept while the workgroup's tasks stay in
+    //     (sweep, chain)); if not published yet, draw the first MH chunks ahead, then wait
+    int npre = 0;
+    const int64_t key = it * g.n_chains + c;
+    if (s_hkey != key) {
+      const double* src = a.hyp2 + ((int64_t)(s & 1) * g.n_chains + c) * HS;
+      if (tid < 64) {
+        if (it == 0) {  // from before this launch
+          Hs[tid] = a.hyper[(int64_t)c * HS + tid];
+          if (tid == 0) s_ready = 1;
+        } else {
+          const double v = ld_wt(src + tid);
+          const bool ok = __all(slot_full(v)) && __shfl(v, H_TAG, 64) == (double)s;  // the sweep tag
+          if (ok) Hs[tid] = v;
+          if (tid == 0) s_ready = ok ? 1u : 0u;
+        }
+      }
+      __syncthreads();
+      if (!s_ready) {
+        if constexpr (NPRE > 0) {
+          if (cu.active) mh_pre_variates<NPRE>(SlotPhilox(k0, k1, cu.gi, (uint32_t)s), g.S, pv);
+          npre = NPRE;
+        }
+        if (tid < 64) {
+          const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+          for (uint32_t poll = 0;; ++poll) {
+            const double v = ld_wt(src + tid);
+            const double tag = __shfl(v, H_TAG, 64);
+            if (__all(slot_full(v)) && tag == (double)s) {
+              Hs[tid] = v;
+              break;
+            }
+            if (wait_expired(a, t0, poll)) {
+              if (tid == 0) s_abort = 1;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+          }
+        }
+      }
+      if (tid == 0) s_hkey = key;
+      __syncthreads();
+      if (s_abort) break;
+    }
+    // (4) MH, finish, block partial, state
+    StatGen<D, K> st{};
+    CustOut<D> out{};
+    const bool stored = is_stored(s, g);
+    if (cu.active) {
+      cust_coeffs<D, K, false>(cu, Hs, exp_tab);
+      const double s00 = Hs[H_S00];
+      const double s11 = Hs[H_S11];
+      const SlotPhilox ph(k0, k1, cu.gi, (uint32_t)s);
+      if constexpr (NPRE > 0) {
+        if (npre > 0) mh_run_pre<NPRE>(cu, pv, s00, s11, g.S, exp_tab);
+      }
+      mh_run<CLV_STRIDE_PIPE != 0>(cu, ph, s00, s11, g.S, exp_tab, npre);
+      out = cust_finish<D, K, false>(cu, a, s, stored, Hs, k0, k1, nullptr, exp_tab, st);
+    }
+    block_reduce_gen<NS, SWEEP_REDUCE_CHUNK>(st, red, tot);
+    if (tid < NS) st_wt(a.blockpart + ((int64_t)c * g.stride + tid) * g.blocks_per_rank + b, tot[tid]);
+    if (cu.active) cust_store<D, K, CL, true>(cu, out, a, c, s, stored, true);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // partial, state, sums landed (each wave its own)
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(a.done + cb, (uint32_t)(it + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // (5) arrivals: the unit's last block forms the unit partial (group_kernel's order)
+    const double* units = a.blockpart;
+    if (bpu > 1) {
+      const int u = b / bpu;
+      const int nbu = (int)min((int64_t)bpu, nb - (int64_t)u * bpu);
+      if (tid == 0) {
+        uint32_t* ctr = a.unit_arrive + (int64_t)c * g.units_per_rank + u;
+        const uint32_t old = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = old == (uint32_t)((it + 1) * nbu - 1) ? 1u : 0u;
+      }
+      __syncthreads();
+      if (s_last) {
+        if (tid < NS) {
+          const double* p = a.blockpart + ((int64_t)c * g.stride + tid) * g.blocks_per_rank + (int64_t)u * bpu;
+          double t = 0.0;
+          int bb = 0;
+          for (; bb + 8 <= bpu; bb += 8) {
+            double v[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v[q] = ld_wt(p + bb + q);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) t += v[q];
+          }
+          for (; bb < bpu; ++bb) t += ld_wt(p + bb);
+          st_wt(a.unitpart + ((int64_t)c * g.stride + tid) * g.units_per_rank + u, t);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __syncthreads();
+      if (!s_last) continue;
+      units = a.unitpart;
+    }
+    if (tid == 0) {
+      const uint32_t old = __hip_atomic_fetch_add(a.chain_arrive + c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = old == (uint32_t)((it + 1) * n_units - 1) ? 1u : 0u;
+    }
+    __syncthreads();
+    if (!s_last) continue;
+    // (6) the chain's last unit: fixed-order sum of every unit partial, the level-2 draw, the
+    //     next sweep's (beta, Sigma) published (or carried out of the launch after its last sweep)
+    const int64_t hs = (D == 2) ? s + 1 : s;
+    if (tid < 64) {  // this draw's variates: drawn after the previous draw of the chain (tagged), else here
+      const double* hv = a.hvar_out + ((int64_t)(s & 1) * g.n_chains + c) * HV;
+      const double v = ld_wt(hv + tid % HV);
+      const bool have = __shfl(v, HV - 1, 64) == (double)hs;
+      double w = v;
+      if (!have) w = stride_hyper_variate<D, K>(a, k0, k1, hs, tid);
+      if (tid < 3) var_iw[tid] = w;
+      else if (tid < 6) var_chi[tid - 3] = w;
+      else if (tid >= 8 && tid < 8 + D * K) var_noise[tid - 8] = w;
+    }
+    double acc[NS];
+    hyper_sum_units<NS, NT>(a.h, c, units, acc);
+    block_reduce<NS, NT>(acc, red, tot);  // (its barriers publish the variates)
+    double* hyp_c = a.hyp2 + (int64_t)c * HS;
+    if (it > 0 && tid < HS) st_wt(hyp_c + (int64_t)(s & 1) * g.n_chains * HS + tid, slot_empty());  // every reader of s has read it
+    level2_draw<D, K>(tot, var_iw, var_chi, var_noise, false, &l2);
+    if (tid < HS) Hs[tid] = 0.0;  // (wavefront 0: ordered before the finalisation's writes)
+    if (tid == 0) {
+      double Sig[D][D];
+#pragma unroll
+      for (int p = 0; p < D; ++p)
+#pragma unroll
+        for (int q = 0; q < D; ++q) Sig[p][q] = l2.Sig[p * D + q];
+      finalize_hyper<D, K, true>(l2.beta, Sig, a.h.omega2, Hs);
+      Hs[H_TAG] = (double)(s + 1);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the reset landed before the publish
+    __syncthreads();
+    const bool last = it == n_sweeps - 1;
+    if (tid < HS) {
+      if (last) a.hyper_out[(int64_t)c * HS + tid] = Hs[tid];
+      else st_wt(hyp_c + (int64_t)((s + 1) & 1) * g.n_chains * HS + tid, Hs[tid]);
+    }
+    const bool store_l2 = hs >= 1 && is_stored(hs, g);
+    double* o = store_l2 ? a.h.level2 + ((int64_t)c * g.n_draws + draw_index(hs, g)) * g.l2w : nullptr;
+    if (tid < K * D && store_l2) o[(tid % D) * K + tid / D] = l2.beta[tid];  // beta.T.ravel() (bi:411)
+    if (tid == 0) {
+      if (store_l2) {
+        int q = K * D;
+#pragma unroll
+        for (int p = 0; p < D; ++p)
+#pragma unroll
+          for (int r = p; r < D; ++r) o[q++] = l2.Sig[p * D + r];  // bi:412, tri:550-554
+      }
+      if (is_stored(s, g)) a.h.loglik[(int64_t)c * g.n_draws + draw_index(s, g)] = tot[NS - 1] / (double)g.n_global;
+      if (last) a.ctrl_rw->cur = s;
+      s_hkey = last ? -1 : key + g.n_chains;  // this workgroup holds (beta, Sigma) of (it + 1, c) already
+    }
+    if (!last && tid < 64) {  // the chain's next draw's variates, off its critical path; the tag last
+      double* hv = a.hvar_out + ((int64_t)((s + 1) & 1) * g.n_chains + c) * HV;
+      const double w = stride_hyper_variate<D, K>(a, k0, k1, hs + 1, tid);
+      if (tid < HV - 1) st_wt(hv + tid, w);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (tid == 0) st_wt(hv + HV - 1, (double)(hs + 1));
+    }
+    __syncthreads();
+  }
+}
+
+template <int D, int K>
+__global__ __launch_bounds__(BLOCK) void stride_kernel(SweepArgs a, int64_t s_first, int64_t n_sweeps) {
+  stride_body<D, K>(a, s_first, n_sweeps);
+}
+template <int D, int K>
+__global__ __launch_bounds__(BLOCK, 4) void stride_kernel_occ4(SweepArgs a, int64_t s_first, int64_t n_sweeps) {
+  stride_body<D, K>(a, s_first, n_sweeps);
+}
+
 // (beta, Sigma) -> hyper state for every chain: [chain][K*D + D*D] input.
 template <int D, int K>
 __global__ void set_hyper_kernel(int n_chains, double* hyper, const double* bs, double omega2) {
@@ -2523,6 +2854,43 @@ hipError_t launch_persist(const SweepArgs& a, int64_t s_first, int64_t n_sweeps,
   CLV_FOR_K(CLV_CASE, 3, false)
   CLV_FOR_K(CLV_CASE, 2, true)
   CLV_FOR_K(CLV_CASE, 3, true)
+#undef CLV_CASE
+  return hipErrorInvalidValue;
+}
+
+template <int D, int K>
+hipError_t launch_stride_t(const SweepArgs& a, int64_t s_first, int64_t n_sweeps, int grid, hipStream_t st,
+                           hipEvent_t e0, hipEvent_t e1) {
+  if constexpr (SweepOcc<D, K>::value >= 4) {
+    if (e0) hipExtLaunchKernelGGL((stride_kernel_occ4<D, K>), dim3(grid), dim3(BLOCK), 0, st, e0, e1, 0, a, s_first, n_sweeps);
+    else hipLaunchKernelGGL((stride_kernel_occ4<D, K>), dim3(grid), dim3(BLOCK), 0, st, a, s_first, n_sweeps);
+  } else {
+    if (e0) hipExtLaunchKernelGGL((stride_kernel<D, K>), dim3(grid), dim3(BLOCK), 0, st, e0, e1, 0, a, s_first, n_sweeps);
+    else hipLaunchKernelGGL((stride_kernel<D, K>), dim3(grid), dim3(BLOCK), 0, st, a, s_first, n_sweeps);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_stride(const SweepArgs& a, int64_t s_first, int64_t n_sweeps, int grid, hipStream_t st,
+                         hipEvent_t e0, hipEvent_t e1) {
+#define CLV_CASE(DD, KK, RR) \
+  if (a.g.D == DD && a.g.K == KK) return launch_stride_t<DD, KK>(a, s_first, n_sweeps, grid, st, e0, e1);
+  CLV_FOR_K(CLV_CASE, 2, 0)
+  CLV_FOR_K(CLV_CASE, 3, 0)
+#undef CLV_CASE
+  return hipErrorInvalidValue;
+}
+
+hipError_t stride_occupancy(int D, int K, int* blocks_per_cu) {
+#define CLV_CASE(DD, KK, RR)                                                                                       \
+  if (D == DD && K == KK) {                                                                                        \
+    if constexpr (SweepOcc<DD, KK>::value >= 4)                                                                    \
+      return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, stride_kernel_occ4<DD, KK>, BLOCK, 0);    \
+    else                                                                                                           \
+      return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, stride_kernel<DD, KK>, BLOCK, 0);         \
+  }
+  CLV_FOR_K(CLV_CASE, 2, 0)
+  CLV_FOR_K(CLV_CASE, 3, 0)
 #undef CLV_CASE
   return hipErrorInvalidValue;
 }
