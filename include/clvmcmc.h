@@ -265,10 +265,11 @@ int clv_debug_wg_map(int32_t n_chains, int32_t nb, int32_t n_cu, int32_t* out);
  * less one slot per 32 CUs (MI355X guide, residency of 256-thread blocks), else 0. */
 int clv_debug_persist_fits(int64_t grid_wgs, int32_t blocks_per_cu, int32_t n_cu);
 /* Host only: the persistent grid's MH-variate producer / consumer roles for n_chains chains of nb
- * customer workgroups on n_cu CUs with n_off chunks per consumer — out[linear workgroup][8]:
- * [0] chunks taken from producers, [1] tasks drawn for others, [2..] tasks (consumer << 4 | chunk);
- * all zero when the placement has no shared CUs to balance. */
-int clv_debug_pc_plan(int32_t n_chains, int32_t nb, int32_t n_cu, int32_t n_off, int32_t* out);
+ * customer workgroups on n_cu CUs with up to n_off chunks per consumer and at most load_x100 / 100
+ * tasks per producer on average (0: no cap) — out[linear workgroup][8]: [0] chunks taken from
+ * producers, [1] tasks drawn for others, [2..] tasks (consumer << 4 | chunk); all zero when the
+ * placement has no shared CUs to balance. */
+int clv_debug_pc_plan(int32_t n_chains, int32_t nb, int32_t n_cu, int32_t n_off, int32_t load_x100, int32_t* out);
 
 /* ---- In-process multi-device runs (SURVEY.md §8b devices=, §8e) ----
  * A group drives the n shards of one problem from one host thread: shards[r] = the sampler of rank

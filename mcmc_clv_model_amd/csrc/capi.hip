@@ -321,39 +321,49 @@ std::vector<int32_t> persist_wg_map(int C, int nb, int n_cu) {
 
 // MH-variate producers / consumers over the placement map above (kernels.hip pc_produce /
 // pc_consume): the customer workgroups of shared CUs (linear [C, P) and n_cu + [C, P), where
-// P = T - n_cu) are consumers that leave their first n_off chunks of drawn-ahead MH variates to
-// the customer workgroups alone on their CUs (linear [P, n_cu) and the level-2 workgroups'
-// partners n_cu + [0, C)), which draw them; tasks are dealt round robin, at most PC_DESC - 2 per
-// producer.  Per-SIMD issue work per sweep at c2 (in units of one wavefront's sweep, v = the
-// variates' share 0.39, 5 chunks): shared 2 (1 - v n_off / 5), alone 1 + 1.66 v n_off / 5 — balanced
-// near n_off = 3 (1.53 and 1.39, from 2 and 1).  Empty if the map is not the paired placement.
-std::vector<int32_t> pc_plan(const std::vector<int32_t>& map, int C, int nb, int n_cu, int n_off) {
+// P = T - n_cu) are consumers that leave their first n_i chunks of drawn-ahead MH variates to
+// customer workgroups OF THE SAME CHAIN alone on their CUs (linear [P, n_cu) and the level-2
+// workgroups' partners n_cu + [0, C)), which draw them right after their own block partial.  Per
+// chain, chunk q goes to the chain's consumers in order (round robin over its producers, at most
+// PC_DESC - 2 tasks each, at most load_x100 / 100 on average when load_x100 > 0), so n_i is the
+// same for all of a chain's consumers or one less.  Same-chain dealing matters: a consumer waits
+// for its producers' sweep, so a producer of another chain couples the chains' paces.  Measured at
+// c2.  Empty if the map is not the paired placement.
+std::vector<int32_t> pc_plan(const std::vector<int32_t>& map, int C, int nb, int n_cu, int n_off, int load_x100) {
   const int T = (int)map.size();
   const int P = T - n_cu;
   std::vector<int32_t> desc;
   if (n_off <= 0 || P <= C || T > 2 * n_cu || T != C * (nb + 1)) return desc;
   for (int c = 0; c < C; ++c)  // the paired placement: level-2 workgroups first (persist_wg_map)
     if (map[c] != ((c << 16) | nb)) return desc;
-  std::vector<int> cons, prod;
-  for (int i = C; i < P; ++i) cons.push_back(i);
-  for (int i = n_cu + C; i < n_cu + P; ++i) cons.push_back(i);
-  for (int i = P; i < n_cu; ++i) prod.push_back(i);
-  for (int i = n_cu; i < n_cu + C; ++i) prod.push_back(i);
-  for (int i : prod)
-    if ((map[i] & 0xFFFF) == nb) return desc;  // (a level-2 workgroup is never a producer)
+  std::vector<std::vector<int>> cons(C), prod(C);
+  for (int i = C; i < P; ++i) cons[map[i] >> 16].push_back(i);
+  for (int i = n_cu + C; i < n_cu + P; ++i) cons[map[i] >> 16].push_back(i);
+  for (int i = P; i < n_cu; ++i) prod[map[i] >> 16].push_back(i);
+  for (int i = n_cu; i < n_cu + C; ++i) prod[map[i] >> 16].push_back(i);
+  for (int c = 0; c < C; ++c)
+    for (int i : prod[c])
+      if ((map[i] & 0xFFFF) == nb) return desc;  // (a level-2 workgroup is never a producer)
   const int per = PC_DESC - 2;
-  while (n_off > 0 && (int64_t)cons.size() * n_off > (int64_t)prod.size() * per) --n_off;
-  if (n_off <= 0 || prod.empty()) return desc;
   desc.assign((size_t)T * PC_DESC, 0);
-  int t = 0;
-  for (int i : cons) {
-    desc[(size_t)i * PC_DESC] = n_off;
-    for (int q = 0; q < n_off; ++q, ++t) {
-      const int p = prod[t % prod.size()];
-      int32_t* d = &desc[(size_t)p * PC_DESC];
-      d[2 + d[1]++] = (i << 4) | q;
-    }
+  bool any = false;
+  for (int c = 0; c < C; ++c) {
+    const std::vector<int>& cs = cons[c];
+    const std::vector<int>& ps = prod[c];
+    if (cs.empty() || ps.empty()) continue;
+    int64_t budget = std::min((int64_t)cs.size() * n_off, (int64_t)ps.size() * per);
+    if (load_x100 > 0) budget = std::min(budget, (int64_t)ps.size() * load_x100 / 100);
+    int64_t t = 0;
+    for (int q = 0; q < n_off && t < budget; ++q)  // chunk by chunk: prefixes [0, n_i) per consumer
+      for (size_t k = 0; k < cs.size() && t < budget; ++k, ++t) {
+        const int i = cs[k];
+        desc[(size_t)i * PC_DESC] = q + 1;
+        int32_t* d = &desc[(size_t)ps[t % ps.size()] * PC_DESC];
+        d[2 + d[1]++] = (i << 4) | q;
+        any = true;
+      }
   }
+  if (!any) desc.clear();
   return desc;
 }
 }  // namespace
@@ -476,10 +486,11 @@ int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* pri
   // resident grid taking (sweep, chain, block) tasks from a ticket counter (CLV_STRIDE=0 opts out:
   // one launch per sweep instead)
   if (!s->replay && cfg->world_size == 1 && nb_local > 0 && !s->persistent) {
-    // default: bivariate (4 waves per SIMD like the sweep kernel); the trivariate stride instance
-    // needs more registers than the sweep kernel's 4 waves per SIMD allow (CLV_STRIDE=1 forces it)
+    // opt-in (CLV_STRIDE=1): measured slower than one launch per sweep at c4 / c5 (93.9 vs 86.2 and
+    // 150 vs 121 us per sweep: the task loop costs registers — the bivariate instance spills at 4
+    // waves per SIMD, the trivariate one runs at 2), DESIGN.md §8
     const char* env = std::getenv("CLV_STRIDE");
-    const bool want = env ? std::string(env) != "0" : g.D == 2;
+    const bool want = env && std::string(env) != "0";
     int bpc = 0;
     hipDeviceProp_t prop{};
     if (want && stride_occupancy(g.D, g.K, &bpc) == hipSuccess && bpc > 0 &&
@@ -576,11 +587,14 @@ int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* pri
       CLV_HIPC(dalloc(&s->d_wgmap, map.size()));
       CLV_HIPC(hipMemcpy(s->d_wgmap, map.data(), sizeof(int32_t) * map.size(), hipMemcpyHostToDevice));
       // world size 1: producer / consumer split of the drawn-ahead MH variates (CLV_PC_CHUNKS:
-      // chunks per consumer, 0 = off); full 4-step chunks of drawn-ahead variates only
+      // chunks per consumer, default 1, 0 = off; c2 at 5,000 sweeps: 0 10.87, 1 10.74, 2 14.0, 3
+      // 15.8 us per sweep); full 4-step chunks of drawn-ahead variates only
       env = std::getenv("CLV_PC_CHUNKS");
-      const int n_off = std::min({env ? std::atoi(env) : 3, g.S / MH_CHUNK_STEPS, PC_CHUNKS});
+      const int n_off = std::min({env ? std::atoi(env) : 1, g.S / MH_CHUNK_STEPS, PC_CHUNKS});
+      const char* load_env = std::getenv("CLV_PC_LOAD");  // average tasks per producer x 100 (0: no cap)
+      const int load_x100 = load_env ? std::atoi(load_env) : 0;
       if (s->persistent && s->pre_variates && g.S <= PC_CHUNKS * MH_CHUNK_STEPS && n_off > 0) {
-        const std::vector<int32_t> desc = pc_plan(map, (int)C, (int)nb_local, s->n_cu, n_off);
+        const std::vector<int32_t> desc = pc_plan(map, (int)C, (int)nb_local, s->n_cu, n_off, load_x100);
         if (!desc.empty()) {
           CLV_HIPC(dalloc(&s->d_pcdesc, desc.size()));
           CLV_HIPC(hipMemcpy(s->d_pcdesc, desc.data(), sizeof(int32_t) * desc.size(), hipMemcpyHostToDevice));
@@ -1423,10 +1437,10 @@ int clv_debug_hyper_variates(uint64_t seed, int32_t chain, uint32_t sweep, doubl
   return CLV_OK;
 }
 
-int clv_debug_pc_plan(int32_t n_chains, int32_t nb, int32_t n_cu, int32_t n_off, int32_t* out) {
+int clv_debug_pc_plan(int32_t n_chains, int32_t nb, int32_t n_cu, int32_t n_off, int32_t load_x100, int32_t* out) {
   if (!out || n_chains < 1 || nb < 0 || n_cu < 1 || n_chains >= (1 << 15) || nb >= (1 << 16))
     return fail(CLV_EINVAL, "bad arguments");
-  const std::vector<int32_t> d = pc_plan(persist_wg_map(n_chains, nb, n_cu), n_chains, nb, n_cu, n_off);
+  const std::vector<int32_t> d = pc_plan(persist_wg_map(n_chains, nb, n_cu), n_chains, nb, n_cu, n_off, load_x100);
   const size_t T = (size_t)n_chains * (nb + 1);
   if (d.empty()) std::fill(out, out + T * PC_DESC, 0);
   else std::copy(d.begin(), d.end(), out);

@@ -2191,6 +2191,24 @@ __device__ __forceinline__ bool pc_consume(const SweepArgs& a, int n_off, int64_
   return true;
 }
 
+// The kernel arguments re-read from the kernarg segment through an opaque pointer: in a loop over
+// tasks the compiler otherwise loads every argument once at entry and keeps them all live in SGPRs
+// (hundreds of SGPR spills into VGPR lanes), instead of scalar loads where they are used.
+__device__ __forceinline__ const SweepArgs& kernargs_fresh() {
+  auto p4 = (const __attribute__((address_space(4))) SweepArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p4));
+  return *(const SweepArgs*)p4;
+}
+
+#ifndef CLV_PERSIST_FRESH_ARGS
+#define CLV_PERSIST_FRESH_ARGS 1
+#endif
+template <bool FRESH>
+__device__ __forceinline__ const SweepArgs& loop_args(const SweepArgs& a) {
+  if constexpr (FRESH) return kernargs_fresh();
+  else return a;
+}
+
 // P2P: world size > 1 with the peer exchange (a separate instance, so that the world-size-1
 // kernel carries none of its registers or LDS).
 template <int D, int K, bool P2P>
@@ -2255,8 +2273,14 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
   if constexpr (D == 3) {
     if (cu.active && pre) zeta_lds[tid] = eta_normal(k0, k1, cu.gi, s_first, exp_tab);
   }
-  const double* hyp_c = a.hyp2 + (int64_t)c * HS;
+  const SweepArgs& a_launch = a;
   for (int64_t it = 0; it < n_sweeps; ++it) {
+    // bivariate: the arguments re-read through an opaque kernarg pointer each sweep (scalar loads
+    // where they are used) instead of held across the loop in SGPRs spilled to VGPR lanes (c2: 140
+    // -> 101 SGPR spills, 10.79 -> 10.72 us per sweep; c3 measured 12.56 -> 12.63, so not there)
+    const SweepArgs& a = loop_args<CLV_PERSIST_FRESH_ARGS && D == 2>(a_launch);
+    const Geometry& g = a.g;
+    const double* hyp_c = a.hyp2 + (int64_t)c * HS;
     // Philox products of the customer counter word are the same every sweep; hoisted out of the
     // loop they were kept live (and spilled, tri K=3) — recomputed per sweep instead (a few VALU)
     if constexpr (CLV_OPAQUE_GI(D)) asm volatile("" : "+v"(cu.gi));
@@ -2322,6 +2346,11 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
 #ifdef CLV_STAMPS
     if (stp && a.stamps) a.stamps[1024 * 8 + wgi * 12 + 11] = blockIdx.y * gridDim.x + blockIdx.x;  // dispatch position
 #endif
+    // producer: consumers' chunks of sweep s + 1 (every lane: the consumer polls all of its lanes),
+    // before this workgroup's own next-sweep work — the consumers need them as soon as (beta, Sigma)
+    // of s + 1 arrive (drawn after the own work: c2 10.83 instead of 10.73 us per sweep)
+    if (pre && it + 1 < n_sweeps)
+      for (int k = 0; k < pc_ntask; ++k) pc_produce(a, a.pc_desc[L_wg * PC_DESC + 2 + k], s + 1, T_wg, tid);
     if (cu.active) {
       cust_store<D, K>(cu, out, a, c, s, stored, false);
       if (it + 1 < n_sweeps) {
@@ -2332,9 +2361,6 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
         }
       }
     }
-    // producer: consumers' chunks of sweep s + 1 (every lane: the consumer polls all of its lanes)
-    if (pre && it + 1 < n_sweeps)
-      for (int k = 0; k < pc_ntask; ++k) pc_produce(a, a.pc_desc[L_wg * PC_DESC + 2 + k], s + 1, T_wg, tid);
     CLV_P_STAMP(a.stamps, wgi, 6, stp);
   }
   if (cu.active) {  // the carried state, once per launch (adopted by the host if nothing aborted)
@@ -2378,15 +2404,6 @@ template <int D, int K>
 struct StridePre {  // MH-variate chunks drawn ahead while (beta, Sigma) are awaited (LDS: 12 KiB each)
   static constexpr int value = CLV_STRIDE_PRE(D);
 };
-
-// The kernel arguments re-read from the kernarg segment through an opaque pointer: in a loop over
-// tasks the compiler otherwise loads every argument once at entry and keeps them all live in SGPRs
-// (hundreds of SGPR spills into VGPR lanes), instead of scalar loads where they are used.
-__device__ __forceinline__ const SweepArgs& kernargs_fresh() {
-  auto p4 = (const __attribute__((address_space(4))) SweepArgs*)__builtin_amdgcn_kernarg_segment_ptr();
-  asm volatile("" : "+s"(p4));
-  return *(const SweepArgs*)p4;
-}
 
 // Lane l of one wavefront: the level-2 draw's Philox variate of record slot l (hyper_variates'
 // layout of the fused path's hvar: [0, 3) inverse-Wishart normals, [3, 6) chi-squares, [8, 8 + DK)
@@ -2435,7 +2452,6 @@ __device__ __forceinline__ void stride_body(const SweepArgs& a0, int64_t s_first
     // were hoisted, kept live and spilled)
     int tid = tid0;
     asm volatile("" : "+v"(tid));
-    const int wave = tid >> 6;
     const Geometry& g = a.g;
     const int64_t nb = g.nb_local;
     const int64_t ntask = (int64_t)g.n_chains * nb;  // tasks per sweep

@@ -508,7 +508,7 @@ def _run_mode(p, persistent, sweeps, chunks, stride=False, **kw):
                                              (3, ["gender_F"], 2357, "summary", 23),
                                              (2, [f"c{k}" for k in range(1, 5)], 3000, "summary", 20),
                                              (3, [f"c{k}" for k in range(1, 9)], 2357, "full", 20)])
-def test_persistent_kernel_bitwise_equals_launch_per_sweep(L, D, covs, n, sink, S):
+def test_persistent_kernel_bitwise_equals_launch_per_sweep(L, monkeypatch, D, covs, n, sink, S):
     """World size 1: the persistent kernel (one launch for all of a clv_run's sweeps, sentinel-slot
     hand-off to a level-2 workgroup per chain) is chosen by default where the grid fits at once,
     and reproduces the launch-per-sweep path (fused level-2 tail) bit for bit — state, draws,
@@ -525,6 +525,8 @@ def test_persistent_kernel_bitwise_equals_launch_per_sweep(L, D, covs, n, sink, 
     p = build_problem(df, covs, D)
     kw = dict(mcmc=25, burnin=6, thin=3, chains=3, seed=2024, draw_sink=sink, n_mh_steps=S)
     chunks = (1, 7, 2, 20, 1)
+    if D == 2 and n == 23570:  # (the producer / consumer split at 3 chunks, beyond its default 1)
+        monkeypatch.setenv("CLV_PC_CHUNKS", "3")
     a = _run_mode(p, True, 31, chunks, **kw)
     b = _run_mode(p, False, 31, chunks, **kw)
     assert a[0]["persistent"] and not b[0]["persistent"], (a[0], b[0])
@@ -572,7 +574,7 @@ def test_stride_kernel_bitwise_equals_launch_per_sweep(L, D, covs, n, chains, si
 def test_producer_consumer_variates_bitwise(L, monkeypatch, chunks):
     """c2's layout (4 chains x 23,570 customers: 376 workgroups on 256 CUs): consumer workgroups on
     shared CUs read their first MH-variate chunks from producer workgroups (CLV_PC_CHUNKS chunks,
-    default 3) — bitwise the same run as without the split (CLV_PC_CHUNKS=0)."""
+    default 1) — bitwise the same run as without the split (CLV_PC_CHUNKS=0)."""
     from mcmc_clv_model_amd.sampler import build_problem
     p = build_problem(cdnow("full"), ["first_sales_scaled"], 2)
     kw = dict(mcmc=12, burnin=8, thin=2, chains=4, seed=31, draw_sink="summary", n_mh_steps=20)
@@ -582,7 +584,9 @@ def test_producer_consumer_variates_bitwise(L, monkeypatch, chunks):
     monkeypatch.setenv("CLV_PC_CHUNKS", chunks)
     got = _run_mode(p, True, 20, (3, 17), **kw)
     assert got[0]["pc_chunks"] == int(chunks), got[0]
-    for x, y in zip(ref[1:], got[1:]):
+    for x, y in zip(ref[1], got[1]):  # state
+        assert np.array_equal(bits(x), bits(y))
+    for x, y in zip(ref[2:], got[2:]):  # draws, level 2, log-likelihood, summaries
         if x is not None:
             assert np.array_equal(bits(x), bits(y))
 

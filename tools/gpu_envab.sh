@@ -4,7 +4,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R; mkdir -p gpurun_out
 ENVS=$1; shift
 for W in "$@"; do
   for E in $ENVS; do
-    env $E timeout -k 10 300 python bench.py --workload $W --no-cpu-baseline --scaling-configs= --no-c1-leg --steps ${STEPS:-5000} \
+    env ${E//,/ } timeout -k 10 300 python bench.py --workload $W --no-cpu-baseline --scaling-configs= --no-c1-leg --steps ${STEPS:-5000} \
       --warmup 300 --timing-steps 500 > gpurun_out/eab_${W}_${E}.log 2>&1; rc=$?
     echo ${W} ${E} rc=$rc; python - "gpurun_out/eab_${W}_${E}.log" <<'PY'
 import json,sys
