@@ -291,6 +291,8 @@ def main():
                     help="BASELINE multi-GPU configurations also measured at this N (c4 strong, c5 weak "
                          "scaling), reported under `configs`; '' to skip")
     ap.add_argument("--scaling-steps", type=int, default=200)
+    ap.add_argument("--blocks-per-unit", type=int, default=0,
+                    help="(world size 1, A/B) blocks per statistics unit instead of the plan's (0)")
     ap.add_argument("--no-c1-leg", dest="c1_leg", action="store_false",
                     help="skip BASELINE configs[0] (c1 on the GPU and its 1-core CPU leg)")
     ap.add_argument("--one-gpu-rehearsal", action="store_true",
@@ -340,7 +342,7 @@ def main():
     if not sharded:
         p = build_problem(df, covs, D)
         s = HipSampler(p, mcmc=mcmc, burnin=burnin, thin=thin, chains=chains, seed=42, draw_sink=sink,
-                       device=local_rank)
+                       device=local_rank, blocks_per_unit=a.blocks_per_unit)
         run = s.run
         sync = s.synchronize
         kern = s
