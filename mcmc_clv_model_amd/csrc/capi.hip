@@ -82,6 +82,7 @@ SweepArgs sweep_args(clv_sampler* s, int init, int fuse = 0) {
   a.wait_ticks = s->wait_ticks;
   a.abort_host = s->d_h_abort;
   a.pre_variates = s->pre_variates;
+  a.prio_mh = s->prio_mh;
   a.h = hyper_args(s, nullptr, 0);
   if (fuse) a.h.hvar = s->replay ? nullptr : s->d_hvar;
   return a;
@@ -284,15 +285,20 @@ std::vector<int32_t> persist_wg_map(int C, int nb, int n_cu) {
     todo[c].pop_back();
   }
   const bool l2_paired = (int)first.size() == C;
+  const char* pair_env = std::getenv("CLV_WG_PAIR");  // (A/B) "cross": pair chain c with chain c + C/2
+  const bool cross = pair_env && std::string(pair_env) == "cross" && C >= 2;
   for (int c = 0; p < P; c = (c + 1) % C) {  // same-chain customer pairs, round robin over chains
+    const int c2 = cross ? (c + C / 2) % C : c;
     bool any = false;
-    for (int k = 0; k < C && !any; ++k) any = todo[(c + k) % C].size() >= 2;
+    for (int k = 0; k < C && !any; ++k)
+      any = cross ? (todo[(c + k) % C].size() >= 1 && todo[((c + k) % C + C / 2) % C].size() >= 1 && (c + k) % C != ((c + k) % C + C / 2) % C)
+                  : todo[(c + k) % C].size() >= 2;
     if (!any) return map;  // cannot pair within chains: keep the identity
-    if (todo[c].size() < 2) continue;
+    if (cross ? (todo[c].empty() || todo[c2].empty() || c == c2) : todo[c].size() < 2) continue;
     first.push_back((c << 16) | todo[c].back());
     todo[c].pop_back();
-    second.push_back((c << 16) | todo[c].back());
-    todo[c].pop_back();
+    second.push_back((c2 << 16) | todo[c2].back());
+    todo[c2].pop_back();
     ++p;
   }
   for (int c = 0; c < C; ++c) {
@@ -575,6 +581,8 @@ int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* pri
     s->timing_record = !(env && std::string(env) == "0");
     env = std::getenv("CLV_PRE_VARIATES");  // 0: MH variates drawn inside the MH phase (A/B)
     s->pre_variates = (env && std::string(env) == "0") ? 0 : 1;
+    env = std::getenv("CLV_PRIO_MH");  // (A/B) s_setprio of the MH phase, 1..3
+    s->prio_mh = env ? std::max(0, std::min(3, std::atoi(env))) : 0;
   }
   if ((s->persistent || s->p2p_capable) && s->n_cu > 0) {
     // default on for the bivariate model only: measured c2 13.44 -> 12.94 us per sweep, but c3

@@ -133,6 +133,7 @@ struct clv_sampler {
   int64_t inflight_n = 0;           // sweeps of the persistent launch in flight (persist_launch)
   hipEvent_t inflight_done = nullptr;  // its end event (null: wait with hipStreamSynchronize)
   int pre_variates = 1;             // CLV_PRE_VARIATES (read at create)
+  int prio_mh = 0;                  // CLV_PRIO_MH (read at create): persistent kernel MH-phase priority
   bool timing_record = true;        // timed persistent launches bracketed by hipEventRecord
                                     // (CLV_TIMING_RECORD=0: the dispatch's own timestamps)
 

@@ -115,6 +115,7 @@ struct SweepArgs {
   int rank;
   const int32_t* wg_map;     // persistent kernel: linear workgroup -> (chain << 16 | block), or null
   int pre_variates;          // persistent kernel: draw the next sweep's MH variates during the hand-off
+  int prio_mh;               // persistent kernel: wave priority (s_setprio) of the MH phase, 0 = off
   // persistent kernel, world size 1: MH-variate producers / consumers (SIMD balancing, capi.hip
   // pc_plan).  pc_desc[linear workgroup][PC_DESC]: [0] chunks of its own next-sweep MH variates
   // this workgroup reads from vbuf instead of drawing them (consumer), [1] number of chunk tasks

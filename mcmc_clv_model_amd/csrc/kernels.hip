@@ -17,6 +17,12 @@
 #include "kernels.h"
 #include "philox.h"
 
+#ifndef CLV_MH_MASKED
+#define CLV_MH_MASKED 1  // MH accept as exec-masked 64-bit moves (mh_step)
+#endif
+#ifndef CLV_MH_THR_ASM
+#define CLV_MH_THR_ASM 0  // (A/B) MH accept threshold as a three-address v_fma_f64: c2 10.65 without, 10.68 with — off
+#endif
 #ifndef SWEEP_MH_PIPELINE
 #define SWEEP_MH_PIPELINE 1  // 1: next MH chunk's variates drawn during the current chunk's steps
 #endif
@@ -1212,15 +1218,44 @@ __device__ __forceinline__ double prop_lm(double a, double b, double c) {
 template <int D, int K, bool CL>
 __device__ __forceinline__ void mh_step(Cust<D, K, CL>& u, double s00, double s11, float t_l, float t_m, float l2u,
                                         const double* exp_tab) {
+#if CLV_MH_THR_ASM
+  // cur + ln2 log2 u as a three-address v_fma_f64 (the compiler's v_fmac form needed a v_mov_b64
+  // copy of cur every step); ln 2 from SGPRs
+  double thr;
+  const double ln2 = 0x1.62e42fefa39efp-1;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(thr) : "v"((double)l2u), "s"(ln2), "v"(u.cur));
+#else
   const double thr = __builtin_fma((double)l2u, 0x1.62e42fefa39efp-1, u.cur);  // cur + ln2 log2 u
+#endif
   const double pl = clip70_fma(s00, (double)t_l, u.ll);
   const double pm = prop_lm(s11, (double)t_m, u.lm);
   const double plp = log_post_fast(u.fc, pl, pm, exp_tab);
+#if CLV_MH_MASKED
+  // The accept as three exec-masked 64-bit moves (3 VALU) instead of six v_cndmask_b32 halves:
+  // exec narrowed to the accepting lanes for the moves and restored inside the one asm block (so
+  // still no branch: the chunk's steps stay one basic block).  Same predicate as below: 5 >= pm
+  // and plp > thr, both false on NaN.
+  uint64_t m0, m1, sv;
+  const double five = 5.0;
+  asm volatile(
+      "v_cmp_ge_f64_e64 %[m0], %[five], %[pm]\n\t"
+      "v_cmp_gt_f64_e64 %[m1], %[plp], %[thr]\n\t"
+      "s_and_saveexec_b64 %[sv], %[m0]\n\t"
+      "s_and_b64 exec, exec, %[m1]\n\t"
+      "v_mov_b64 %[ll], %[pl]\n\t"
+      "v_mov_b64 %[lm], %[pm]\n\t"
+      "v_mov_b64 %[cur], %[plp]\n\t"
+      "s_mov_b64 exec, %[sv]"
+      : [ll] "+v"(u.ll), [lm] "+v"(u.lm), [cur] "+v"(u.cur), [m0] "=&s"(m0), [m1] "=&s"(m1), [sv] "=&s"(sv)
+      : [pl] "v"(pl), [pm] "v"(pm), [plp] "v"(plp), [thr] "v"(thr), [five] "s"(five)
+      : "scc");
+#else
   // selects, not a branch: keeps a chunk's steps in one basic block with the next chunk's variates
   const bool acc = (pm <= 5.0) & (plp > thr);
   u.ll = acc ? pl : u.ll;
   u.lm = acc ? pm : u.lm;
   u.cur = acc ? plp : u.cur;
+#endif
 }
 
 // The sweep's S Philox-mode MH steps.  Software pipeline: the Philox blocks and t3 transforms of
@@ -2209,6 +2244,14 @@ __device__ __forceinline__ const SweepArgs& loop_args(const SweepArgs& a) {
   else return a;
 }
 
+// Wave priority (s_setprio) for the persistent kernel's MH-phase experiment (SweepArgs::prio_mh).
+__device__ __forceinline__ void set_prio(int p) {
+  if (p == 3) __builtin_amdgcn_s_setprio(3);
+  else if (p == 2) __builtin_amdgcn_s_setprio(2);
+  else if (p == 1) __builtin_amdgcn_s_setprio(1);
+  else __builtin_amdgcn_s_setprio(0);
+}
+
 // P2P: world size > 1 with the peer exchange (a separate instance, so that the world-size-1
 // kernel carries none of its registers or LDS).
 template <int D, int K, bool P2P>
@@ -2250,6 +2293,7 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
   if (tid == 0) s_abort = 0;
 
   if (b == g.nb_local) {  // the chain's level-2 workgroup
+    if (a.prio_mh) set_prio(3);  // (experiment) the draw is on every chain's critical path
     persist_level2<D, K, P2P>(a, s_first, n_sweeps, c, k0, k1, wgi, it_stamp, (double*)pool);
     return;
   }
@@ -2312,6 +2356,7 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
       if (s_abort) return;
     }
     CLV_P_STAMP(a.stamps, wgi, 1, stp);
+    if (a.prio_mh) set_prio(a.prio_mh);  // (experiment) MH phase ahead of a co-resident wave's variates
     StatGen<D, K> st{};
     CustOut<D> out{};
     if (cu.active) {
@@ -2340,6 +2385,7 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
     }
 #endif
     if (tid < NS) st_wt(parts + (int64_t)b * NS + tid, tot[tid]);  // one contiguous 8*NS-byte record
+    if (a.prio_mh) set_prio(0);
     CLV_P_STAMP(a.stamps, wgi, 5, stp);
     CLV_P_STAMP(a.stamps, wgi, 8, stp);
     CLV_P_STAMP(a.stamps, wgi, 9, stp);

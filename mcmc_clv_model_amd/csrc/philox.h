@@ -156,6 +156,36 @@ __device__ __forceinline__ float t3_f32(float u, float v) {
 __device__ __forceinline__ float angle_hi(uint32_t w) { return (float)(w >> 16) * 0x1.0p-16f; }
 __device__ __forceinline__ float angle_lo(uint32_t w) { return (float)(w & 0xffffu) * 0x1.0p-16f; }
 
+// The step's two t3 variates (t_l from words x and z's high half, t_m from y and z's low half)
+// with every non-transcendental operation on the PAIR in one packed fp32 instruction
+// (v_pk_fma_f32 / v_pk_mul_f32: two lanes' worth per issue): the same IEEE operations in the same
+// order as two t3_f32 calls, so the same bits, in 17 VALU instead of 21.
+#ifndef CLV_T3_PACKED
+#define CLV_T3_PACKED 0  // measured at c2: 10.80 -> 10.87 us per sweep (packed) — off
+#endif
+#if defined(__clang__)  // (clang vector extension; the header is also host-compiled by g++ in tests)
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 t3_pair(uint32_t wl, uint32_t wm, uint32_t wz) {
+  const f32x2 c32 = {0x1.0p-32f, 0x1.0p-32f}, c33 = {0x1.0p-33f, 0x1.0p-33f};
+  const f32x2 m23 = {-(2.0f / 3.0f), -(2.0f / 3.0f)}, three = {3.0f, 3.0f}, mthree = {-3.0f, -3.0f};
+  const f32x2 a16 = {0x1.0p-16f, 0x1.0p-16f};
+  f32x2 u = {(float)wl, (float)wm};
+  u = __builtin_elementwise_fma(u, c32, c33);                       // uf32 of both radius words
+  f32x2 lg = {__builtin_amdgcn_logf(u.x), __builtin_amdgcn_logf(u.y)};
+  lg = lg * m23;
+  f32x2 p = {__builtin_amdgcn_exp2f(lg.x), __builtin_amdgcn_exp2f(lg.y)};  // U^(-2/3)
+  p = __builtin_elementwise_fma(three, p, mthree);                  // 3 (p - 1), one rounding
+  f32x2 ang = {(float)(wz >> 16), (float)(wz & 0xffffu)};
+  ang = ang * a16;
+  const f32x2 r = {__builtin_amdgcn_sqrtf(p.x), __builtin_amdgcn_sqrtf(p.y)};
+  const f32x2 cs = {__builtin_amdgcn_cosf(ang.x), __builtin_amdgcn_cosf(ang.y)};
+  return r * cs;
+}
+#else
+#undef CLV_T3_PACKED
+#define CLV_T3_PACKED 0
+#endif
+
 // Words of the MH steps: step j uses the four words of Philox block SLOT_MH0 + j:
 // x = radius uniform of t_l, y = radius uniform of t_m, z = the two angles (16 bits each),
 // w = accept uniform.  Chunk q = steps 4q .. 4q+3.
@@ -206,8 +236,14 @@ __device__ __forceinline__ void mh_chunk_variates(const PH& ph, uint32_t q, floa
 #pragma unroll
   for (int i = 0; i < MH_CHUNK_STEPS; ++i) {
     const u32x4 r = ph(SLOT_MH0 + (uint32_t)MH_CHUNK_STEPS * q + (uint32_t)i);
+#if CLV_T3_PACKED && !defined(CLV_T3_CHEAP)
+    const f32x2 t = t3_pair(r.x, r.y, r.z);
+    t_l[i] = t.x;
+    t_m[i] = t.y;
+#else
     t_l[i] = t3_f32(uf32(r.x), angle_hi(r.z));
     t_m[i] = t3_f32(uf32(r.y), angle_lo(r.z));
+#endif
     log2_u[i] = log2_f32(uf32(r.w));
   }
 }

@@ -53,6 +53,18 @@ def main(workload="c2", sweeps=1500):
                     finish=(cust[:, 4] - cust[:, 3])[act], store=cust[:, 5] - cust[:, 4], next=cust[:, 6] - cust[:, 5])
         txt = "  ".join(f"{n} {np.median(v) * us:5.2f}/{v.max() * us:5.2f}" for n, v in cols.items())
         print(f"  chain {c} (median/max us): {txt}")
+        # by placement: workgroups on shared CUs (linear dispatch position < P or >= n_cu) vs alone
+        T, ncu = info["workgroups"], info["n_cu"]
+        pos = cust[:, 11]
+        shared = (pos < T - ncu) | (pos >= ncu)
+        for tag, m in (("shared", shared), ("alone ", ~shared)):
+            if not m.any():
+                continue
+            ph = dict(top=cust[m, 0] - R, observe=cust[m, 1] - R, MH=cust[m, 3] - cust[m, 2], finish=cust[m, 4] - cust[m, 3],
+                      store=cust[m, 5] - cust[m, 4], next=cust[m, 6] - cust[m, 5], partial=cust[m, 5] - R,
+                      nextdone=cust[m, 6] - R)
+            print(f"    {tag} x{int(m.sum()):3d} (median/max us): " +
+                  "  ".join(f"{n} {np.median(v) * us:5.2f}/{v.max() * us:5.2f}" for n, v in ph.items()))
         print(f"    last partial issued {(cust[:, 5].max() - R) * us:6.2f}  tail: variates {(tail[1] - tail[0]) * us:5.2f}"
               f"  partials seen {(tail[2] - R) * us:6.2f}  draw {(tail[3] - tail[2]) * us:5.2f} (reduce {(tail[6] - tail[2]) * us:4.2f}"
               f" algebra {(tail[7] - tail[6]) * us:4.2f} finalize {(tail[3] - tail[7]) * us:4.2f})"
