@@ -44,6 +44,14 @@ __global__ void kern(uint64_t* out, float* fo, double* dout, uint32_t seed) {
         d[i] = d[i] + 1e-7;
       } else if constexpr (OP == 10) {  // v_mul_f64
         d[i] = d[i] * 0.9999999;
+      } else if constexpr (OP == 11) {  // v_exp_f32
+        f[i] = __builtin_amdgcn_exp2f(f[i] - 0.5f);
+      } else if constexpr (OP == 12) {  // v_sqrt_f32
+        f[i] = __builtin_amdgcn_sqrtf(f[i] + 0.25f);
+      } else if constexpr (OP == 13) {  // v_cos_f32 (revolutions)
+        f[i] = __builtin_amdgcn_cosf(f[i] * 0.5f);
+      } else if constexpr (OP == 14) {  // v_add_f32 chain
+        f[i] = f[i] + 1e-4f;
       }
     }
   }
@@ -99,5 +107,9 @@ int main() {
   run<8>("mul_lo_u32 + xor + shr", 3);
   run<9>("v_add_f64", 1);
   run<10>("v_mul_f64", 1);
+  run<11>("v_exp_f32 + add", 2);
+  run<12>("v_sqrt_f32 + add", 2);
+  run<13>("v_cos_f32 + mul", 2);
+  run<14>("v_add_f32", 1);
   return 0;
 }
