@@ -1271,20 +1271,23 @@ __device__ __forceinline__ void mh_run(Cust<D, K, CL>& cu, const SlotPhilox& ph,
   const int n_chunks = (S + MC - 1) / MC;
   if (n_chunks <= q0) return;
   float tl[MC], tm[MC], lu[MC];
+  // trivariate launch-per-sweep instances (c5): the packed t3 pair — c5 122.8 -> 121.6 us per sweep,
+  // bitwise the same variates (the persistent kernels keep the scalar form: c2 measured slower)
+  constexpr bool PK = D == 3 || CLV_T3_PACKED != 0;
   if constexpr (!PIPE) {
   // no software pipeline (occupancy hides the latency instead): variates, then the chunk's steps
   for (int ch = q0; ch < n_chunks; ++ch) {
-    mh_chunk_variates(ph, (uint32_t)ch, tl, tm, lu);
+    mh_chunk_variates<PK>(ph, (uint32_t)ch, tl, tm, lu);
     const int rem = S - ch * MC;
 #pragma unroll
     for (int st = 0; st < MC; ++st) mh_step(cu, s00, s11, tl[st], tm[st], st < rem ? lu[st] : __builtin_inff(), exp_tab);
   }
   return;
   }
-  mh_chunk_variates(ph, (uint32_t)q0, tl, tm, lu);
+  mh_chunk_variates<PK>(ph, (uint32_t)q0, tl, tm, lu);
   for (int ch = q0; ch + 1 < n_chunks; ++ch) {
     float ntl[MC], ntm[MC], nlu[MC];
-    mh_chunk_variates(ph, (uint32_t)(ch + 1), ntl, ntm, nlu);
+    mh_chunk_variates<PK>(ph, (uint32_t)(ch + 1), ntl, ntm, nlu);
 #pragma unroll
     for (int st = 0; st < MC; ++st) mh_step(cu, s00, s11, tl[st], tm[st], lu[st], exp_tab);
 #pragma unroll

@@ -161,8 +161,8 @@ __device__ __forceinline__ float angle_lo(uint32_t w) { return (float)(w & 0xfff
 // (v_pk_fma_f32 / v_pk_mul_f32: two lanes' worth per issue): the same IEEE operations in the same
 // order as two t3_f32 calls, so the same bits, in 17 VALU instead of 21.
 #ifndef CLV_T3_PACKED
-#define CLV_T3_PACKED 0  // measured at c2: 10.80 -> 10.87 us per sweep (packed) — off
-#endif
+#define CLV_T3_PACKED 0  // default of every call site but mh_run's trivariate instances: measured at c2
+#endif                   // 10.80 -> 10.87 us per sweep and c4 85.0 -> 87.2 (packed); c5 122.8 -> 121.6
 #if defined(__clang__)  // (clang vector extension; the header is also host-compiled by g++ in tests)
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f32x2 t3_pair(uint32_t wl, uint32_t wm, uint32_t wz) {
@@ -207,7 +207,7 @@ __device__ __forceinline__ float uf24(uint32_t w) {  // (k + 1) 2^-24, k = w[23:
 __device__ __forceinline__ float angle12(uint32_t hi8_word, uint32_t lo4) {  // (hi8 . lo4) 2^-12
   return __builtin_fmaf((float)(hi8_word >> 24), 0x1.0p-8f, (float)lo4 * 0x1.0p-12f);
 }
-template <class PH>
+template <bool PACKED = false, class PH>  // (PACKED: unused here)
 __device__ __forceinline__ void mh_chunk_variates(const PH& ph, uint32_t q, float (&t_l)[4], float (&t_m)[4],
                                                   float (&log2_u)[4]) {
   uint32_t W[12];
@@ -229,17 +229,23 @@ __device__ __forceinline__ void mh_chunk_variates(const PH& ph, uint32_t q, floa
 }
 #else
 constexpr int MH_BLOCKS_PER_CHUNK = 4;
-// One chunk's variates: t_l, t_m and log2(U_accept) of 4 consecutive MH steps.
-template <class PH>
+// One chunk's variates: t_l, t_m and log2(U_accept) of 4 consecutive MH steps.  PACKED: the pair
+// of t3 transforms as t3_pair (the same bits; the launch-per-sweep trivariate kernel takes it)
+template <bool PACKED = (CLV_T3_PACKED != 0), class PH>
 __device__ __forceinline__ void mh_chunk_variates(const PH& ph, uint32_t q, float (&t_l)[4], float (&t_m)[4],
                                                   float (&log2_u)[4]) {
 #pragma unroll
   for (int i = 0; i < MH_CHUNK_STEPS; ++i) {
     const u32x4 r = ph(SLOT_MH0 + (uint32_t)MH_CHUNK_STEPS * q + (uint32_t)i);
-#if CLV_T3_PACKED && !defined(CLV_T3_CHEAP)
-    const f32x2 t = t3_pair(r.x, r.y, r.z);
-    t_l[i] = t.x;
-    t_m[i] = t.y;
+#if defined(__clang__) && !defined(CLV_T3_CHEAP)
+    if constexpr (PACKED) {
+      const f32x2 t = t3_pair(r.x, r.y, r.z);
+      t_l[i] = t.x;
+      t_m[i] = t.y;
+    } else {
+      t_l[i] = t3_f32(uf32(r.x), angle_hi(r.z));
+      t_m[i] = t3_f32(uf32(r.y), angle_lo(r.z));
+    }
 #else
     t_l[i] = t3_f32(uf32(r.x), angle_hi(r.z));
     t_m[i] = t3_f32(uf32(r.y), angle_lo(r.z));
