@@ -1535,7 +1535,7 @@ __device__ __forceinline__ void sweep_body(const SweepArgs& a) {
   static_assert(BLOCK == EXP_TAB_N && BLOCK == LOG_TAB_N && BLOCK == COS_TAB_N, "one table entry per thread");
   double tab_v = 0.0, tab_l0 = 0.0, tab_l1 = 0.0, tab_c0 = 0.0, tab_c1 = 0.0;
   if (!REPLAY) {
-    tab_v = EXP2_TAB[threadIdx.x];
+    tab_v = exp_tab_entry(threadIdx.x);
     tab_l0 = LOG_TAB[2 * threadIdx.x];
     tab_l1 = LOG_TAB[2 * threadIdx.x + 1];
     if constexpr (D == 3) {
