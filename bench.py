@@ -247,7 +247,6 @@ def measure_config(name: str, world: int, rank: int, local_rank: int, dist, step
         dt = float(t.item())
     linfo = kern.launch_info()
     persistent = linfo["persistent"]
-    stride_k = linfo.get("stride_grid", 0) > 0
     exch = getattr(kern, "exchange", None)
     note = getattr(kern, "p2p_note", None)
     kern.close()
@@ -262,8 +261,7 @@ def measure_config(name: str, world: int, rank: int, local_rank: int, dist, step
                 n_customers=n_total, customers_per_gpu=n_total // world, chains=chains, steps=steps, warmup=warmup,
                 ms_per_step=dt / steps * 1e3, draw_sink=sink,
                 hbm_frac=round(bpu * value / 1e9 / (world * HBM_PEAK_GBS), 5), bytes_per_unit=round(bpu, 2),
-                path=("persistent kernel" if persistent else "stride kernel (one launch, resident grid)" if stride_k
-                      else "launch-per-sweep sweep kernel") +
+                path=("persistent kernel" if persistent else "launch-per-sweep sweep kernel") +
                      ("" if world == 1 else
                       (", unit partials stored into every rank's mail over xGMI by the kernel (no host collective)"
                        if exch == "p2p" else ", RCCL all-gather + level-2 kernel per sweep") +
@@ -360,8 +358,7 @@ def main():
     timing = not a.no_kernel_timing
     info = kern.launch_info()
     persistent = info["persistent"]
-    stride = info.get("stride_grid", 0) > 0 and not sharded
-    one_launch = persistent or stride   # all sweeps of a clv_run in one launch
+    one_launch = persistent   # all sweeps of a clv_run in one launch
     p2p = sharded and persistent
     run(a.warmup)
     sync()
@@ -421,14 +418,12 @@ def main():
             t_launch = t_sweep * spl
             units = chains * n_local * spl               # (chain, customer) sweeps per launch
             achieved = bpu * units / t_launch / 1e9
-            kname = "persist_kernel" if persistent else ("stride_kernel" if stride else "sweep_kernel")
+            kname = "persist_kernel" if persistent else "sweep_kernel"
             roofline = dict(bound=None, achieved=round(achieved, 3), peak=HBM_PEAK_GBS, unit="GB/s",
                             frac=round(achieved / HBM_PEAK_GBS, 6), traffic=None,
                             kernel=("persist_kernel (one launch for all sweeps of a clv_run; level-2 workgroup "
                                     "per chain" + ("; unit partials exchanged over xGMI" if p2p else "") + ")")
                             if persistent else
-                            (f"stride_kernel (one launch for all sweeps of a clv_run; {info['stride_grid']} resident "
-                             "workgroups taking (sweep, chain, block) tasks in order)") if stride else
                             ("sweep_kernel (incl. fused level-2 tail)" if not sharded else "sweep_kernel"),
                             bytes_per_unit=round(bpu, 3), units_per_launch=units, sweeps_per_launch=spl,
                             launch_us=round(t_launch * 1e6, 3), sweep_kernel_us=round(t_sweep * 1e6, 3),
@@ -495,7 +490,6 @@ def main():
                         n_customers=n_total, chains=chains, n_mh_steps=20, burnin=burnin, mcmc=mcmc_workload,
                         thin=thin, seed=42, draw_sink=sink, parallelism=f"customer-shard x{world}",
                         timed_region=(f"one persistent-kernel launch of {a.steps} sweeps" if persistent else
-                                      f"one stride-kernel launch of {a.steps} sweeps" if stride else
                                       "hipGraph replay of fused sweep launches") if not sharded else
                         (f"one persistent-kernel launch of {a.steps} sweeps per rank, unit partials stored into "
                          "every rank's IPC-mapped mail over xGMI (no host collective per sweep)") if p2p else

@@ -17,8 +17,10 @@
  *    caller-owned, contiguous, preallocated host buffers (float64, C order).
  *  - A sampler handle belongs to one host thread and one HIP device.
  *  - Customer data is struct-of-arrays: one contiguous array per CBS column.
- *  - All hot-path arithmetic is float64, like the reference; Philox proposal noise is
- *    generated in float32.
+ *  - State, log posteriors and the level-2 draw are float64, like the reference.  In Philox mode
+ *    the MH proposal noise t3 is generated in float32 (fp32 hardware transcendentals), and the
+ *    accept test compares in float64 against cur + ln2 * log2(U) with log2(U) an fp32 v_log_f32
+ *    (DESIGN.md §5); replay mode (tests) takes the reference's own float64 variates.
  */
 #ifndef CLVMCMC_H
 #define CLVMCMC_H
@@ -148,12 +150,11 @@ int clv_synchronize(clv_sampler* s);
 int64_t clv_sweeps_done(const clv_sampler* s);
 /* How clv_run launches: out[6] = (persistent 0/1, persistent-kernel workgroups per CU, CUs,
  * workgroups per sweep, MH-variate chunks each consumer workgroup takes from producer workgroups
- * (0: no producer / consumer split; CLV_PC_CHUNKS), stride-kernel workgroups (0: none)).
+ * (0: no producer / consumer split; CLV_PC_CHUNKS), reserved (0)).
  * Persistent = one launch for all of a clv_run's sweeps with every customer block resident, chosen
  * at create when world_size == 1, Philox mode, every workgroup fits at once (with a residency
- * margin), and CLV_PERSISTENT != "0".  Otherwise at world size 1 in Philox mode the stride kernel
- * (CLV_STRIDE != "0"): one launch for all sweeps too, a resident grid taking (sweep, chain, block)
- * tasks in order with the state in HBM; else one launch per sweep. */
+ * margin), and CLV_PERSISTENT != "0".  Otherwise one launch of the sweep kernel per sweep (fused
+ * level-2 tail), replayed from captured hipGraph chunks. */
 int clv_launch_info(const clv_sampler* s, int64_t* out);
 /* Sharded runs without a host collective per sweep (world_size > 1, Philox mode): the persistent
  * kernel's level-2 workgroup of each chain writes this rank's unit partials of sweep s straight into

@@ -70,8 +70,6 @@ SweepArgs sweep_args(clv_sampler* s, int init, int fuse = 0) {
   a.stamps = s->d_stamps;
   a.mail = s->d_mail;
   a.peers = s->d_peers;
-  a.ticket = s->d_ticket;
-  a.done = s->d_done;
   a.wg_map = s->d_wgmap;
   a.pc_desc = s->d_pcdesc;
   a.vbuf = s->d_vbuf;
@@ -82,7 +80,6 @@ SweepArgs sweep_args(clv_sampler* s, int init, int fuse = 0) {
   a.wait_ticks = s->wait_ticks;
   a.abort_host = s->d_h_abort;
   a.pre_variates = s->pre_variates;
-  a.prio_mh = s->prio_mh;
   a.h = hyper_args(s, nullptr, 0);
   if (fuse) a.h.hvar = s->replay ? nullptr : s->d_hvar;
   return a;
@@ -285,20 +282,15 @@ std::vector<int32_t> persist_wg_map(int C, int nb, int n_cu) {
     todo[c].pop_back();
   }
   const bool l2_paired = (int)first.size() == C;
-  const char* pair_env = std::getenv("CLV_WG_PAIR");  // (A/B) "cross": pair chain c with chain c + C/2
-  const bool cross = pair_env && std::string(pair_env) == "cross" && C >= 2;
   for (int c = 0; p < P; c = (c + 1) % C) {  // same-chain customer pairs, round robin over chains
-    const int c2 = cross ? (c + C / 2) % C : c;
     bool any = false;
-    for (int k = 0; k < C && !any; ++k)
-      any = cross ? (todo[(c + k) % C].size() >= 1 && todo[((c + k) % C + C / 2) % C].size() >= 1 && (c + k) % C != ((c + k) % C + C / 2) % C)
-                  : todo[(c + k) % C].size() >= 2;
+    for (int k = 0; k < C && !any; ++k) any = todo[(c + k) % C].size() >= 2;
     if (!any) return map;  // cannot pair within chains: keep the identity
-    if (cross ? (todo[c].empty() || todo[c2].empty() || c == c2) : todo[c].size() < 2) continue;
+    if (todo[c].size() < 2) continue;
     first.push_back((c << 16) | todo[c].back());
     todo[c].pop_back();
-    second.push_back((c2 << 16) | todo[c2].back());
-    todo[c2].pop_back();
+    second.push_back((c << 16) | todo[c].back());
+    todo[c].pop_back();
     ++p;
   }
   for (int c = 0; c < C; ++c) {
@@ -475,7 +467,7 @@ int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* pri
   CLV_HIPC(dalloc(&s->d_prior, PRIOR_DOUBLES));
   CLV_HIPC(dalloc(&s->d_ctrl, 1));
   CLV_HIPC(dalloc(&s->d_arrive, C + C * (int64_t)g.units_per_rank));  // chain, then unit counters
-  CLV_HIPC(dalloc(&s->d_hvar, 2 * C * HV));  // (the stride kernel uses both sweep-parity sets)
+  CLV_HIPC(dalloc(&s->d_hvar, 2 * C * HV));
   CLV_HIPC(dalloc(&s->d_hyp2, 2 * C * HS));
   // Persistent sweeps (one launch runs many sweeps) when every workgroup of the grid can be
   // resident at once — the chain hand-off spins on the other workgroups (CLV_PERSISTENT=0 opts out)
@@ -487,28 +479,6 @@ int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* pri
       s->n_cu = prop.multiProcessorCount;
     if ((!env || std::string(env) != "0") && persist_grid_fits((int64_t)(nb_local + 1) * C, s->persist_bpc, s->n_cu))
       s->persistent = true;
-  }
-  // Grids too large to be resident at once (world size 1, Philox mode): the stride kernel, a
-  // resident grid taking (sweep, chain, block) tasks from a ticket counter (CLV_STRIDE=0 opts out:
-  // one launch per sweep instead)
-  if (!s->replay && cfg->world_size == 1 && nb_local > 0 && !s->persistent) {
-    // opt-in (CLV_STRIDE=1): measured slower than one launch per sweep at c4 / c5 (93.9 vs 86.2 and
-    // 150 vs 121 us per sweep: the task loop costs registers — the bivariate instance spills at 4
-    // waves per SIMD, the trivariate one runs at 2), DESIGN.md §8
-    const char* env = std::getenv("CLV_STRIDE");
-    const bool want = env && std::string(env) != "0";
-    int bpc = 0;
-    hipDeviceProp_t prop{};
-    if (want && stride_occupancy(g.D, g.K, &bpc) == hipSuccess && bpc > 0 &&
-        hipGetDeviceProperties(&prop, s->device) == hipSuccess) {
-      s->n_cu = prop.multiProcessorCount;
-      int64_t G = (int64_t)C * nb_local;
-      // largest grid that fits with the residency margin (persist_grid_fits)
-      int64_t hi = (int64_t)bpc * s->n_cu;
-      while (hi > 0 && !persist_grid_fits(hi, bpc, s->n_cu)) --hi;
-      G = std::min(G, hi);
-      if (G > 0) s->stride_grid = (int)G;
-    }
   }
   // World size > 1: the same persistent kernel exchanging unit partials with its peers over xGMI
   // (clv_p2p_connect) when the grid fits at once here, as above, and on every rank (the caller
@@ -552,11 +522,7 @@ int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* pri
     CLV_HIPC(hipMemsetAsync(s->d_mail, 0xFF, sizeof(double) * nm, s->stream));  // every slot empty
     CLV_HIPC(dalloc(&s->d_peers, g.world_size));
   }
-  if (s->stride_grid > 0) {
-    CLV_HIPC(dalloc(&s->d_ticket, 1));
-    CLV_HIPC(dalloc(&s->d_done, (size_t)C * nb_local));
-  }
-  if (s->persistent || s->p2p_capable || s->fx_capable || s->stride_grid > 0) {  // (fused exchange / stride: the snapshot buffers)
+  if (s->persistent || s->p2p_capable || s->fx_capable) {  // (fused exchange: the snapshot buffers)
     CLV_HIPC(dalloc(&s->d_pblock, (size_t)C * std::max(nb_local, 1) * g.stride));
     CLV_HIPC(dalloc(&s->d_lam_alt, C * std::max<int64_t>(n, 1)));
     CLV_HIPC(dalloc(&s->d_mu_alt, C * std::max<int64_t>(n, 1)));
@@ -570,7 +536,6 @@ int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* pri
     // resident, so a wait that long means a fault), 10 s with peers (host-side launch skew between
     // ranks); CLV_WAIT_TIMEOUT_MS overrides
     const char* env = std::getenv("CLV_WAIT_TIMEOUT_MS");
-    // (stride kernel: a block's next task may wait for the chain's whole sweep; 2 s is >> a sweep)
     const double ms = env ? std::atof(env) : (cfg->world_size > 1 ? 10000.0 : 2000.0);
     s->wait_ticks = (uint64_t)(std::max(1.0, ms) * 1e5);  // s_memrealtime: 100 MHz
   }
@@ -581,8 +546,6 @@ int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* pri
     s->timing_record = !(env && std::string(env) == "0");
     env = std::getenv("CLV_PRE_VARIATES");  // 0: MH variates drawn inside the MH phase (A/B)
     s->pre_variates = (env && std::string(env) == "0") ? 0 : 1;
-    env = std::getenv("CLV_PRIO_MH");  // (A/B) s_setprio of the MH phase, 1..3
-    s->prio_mh = env ? std::max(0, std::min(3, std::atoi(env))) : 0;
   }
   if ((s->persistent || s->p2p_capable) && s->n_cu > 0) {
     // default on for the bivariate model only: measured c2 13.44 -> 12.94 us per sweep, but c3
@@ -599,8 +562,7 @@ int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* pri
       // 15.8 us per sweep); full 4-step chunks of drawn-ahead variates only
       env = std::getenv("CLV_PC_CHUNKS");
       const int n_off = std::min({env ? std::atoi(env) : 1, g.S / MH_CHUNK_STEPS, PC_CHUNKS});
-      const char* load_env = std::getenv("CLV_PC_LOAD");  // average tasks per producer x 100 (0: no cap)
-      const int load_x100 = load_env ? std::atoi(load_env) : 0;
+      const int load_x100 = 0;  // (no cap on a producer's tasks: capping measured slower)
       if (s->persistent && s->pre_variates && g.S <= PC_CHUNKS * MH_CHUNK_STEPS && n_off > 0) {
         const std::vector<int32_t> desc = pc_plan(map, (int)C, (int)nb_local, s->n_cu, n_off, load_x100);
         if (!desc.empty()) {
@@ -728,8 +690,6 @@ void clv_destroy(clv_sampler* s) {
   if (s->d_peers) (void)hipFree(s->d_peers);
   if (s->d_wgmap) (void)hipFree(s->d_wgmap);
   if (s->d_pcdesc) (void)hipFree(s->d_pcdesc);
-  if (s->d_ticket) (void)hipFree(s->d_ticket);
-  if (s->d_done) (void)hipFree(s->d_done);
   if (s->d_vbuf) (void)hipFree(s->d_vbuf);
   if (s->own_stream && s->own) (void)hipStreamDestroy(s->own);
   delete s;
@@ -822,7 +782,7 @@ int clv_launch_info(const clv_sampler* s, int64_t* out) {
   out[2] = s->n_cu;
   out[3] = (int64_t)(s->g.nb_local + (s->persistent ? 1 : 0)) * s->g.n_chains;
   out[4] = s->pc_chunks;
-  out[5] = s->stride_grid;
+  out[5] = 0;  // (reserved: was the stride kernel's grid, removed)
   return CLV_OK;
 }
 
@@ -1031,73 +991,6 @@ int run_persistent(clv_sampler* s, int64_t n_sweeps) {
   return persist_wait(s);
 }
 
-// Stride kernel (kernels.hip stride_body): launches of up to the ticket counter's range of sweeps.
-// The state is updated in place, so a launch in which a wait timed out is undone from copies taken
-// before it (lambda, mu, running sums); (beta, Sigma) leave through hyper_out as in the persistent
-// path.  Every hand-off slot is empty after a completed launch; counters are zeroed per launch.
-int run_stride(clv_sampler* s, int64_t n_sweeps) {
-  const Geometry& g = s->g;
-  s->last_persist_n = 0;
-  const int64_t ntask = (int64_t)g.n_chains * g.nb_local;
-  const int64_t max_per_launch = std::max<int64_t>(1, (int64_t)(0xFFFFFFFFull - (uint64_t)s->stride_grid - 1) / ntask);
-  const size_t nl = sizeof(double) * (size_t)g.n_chains * std::max<int64_t>(g.n, 1);
-  const size_t sums_bytes = sizeof(double) * (size_t)g.n_chains * CLV_N_SUM_STATS * g.n;
-  const size_t n_arrive = (size_t)g.n_chains + (size_t)g.n_chains * g.units_per_rank;
-  while (n_sweeps > 0) {
-    const int64_t n = std::min(n_sweeps, max_per_launch);
-    if (s->slots_dirty) {
-      CLV_HIP(hipMemsetAsync(s->d_hyp2, 0xFF, sizeof(double) * 2 * g.n_chains * HS, s->stream));
-      s->slots_dirty = false;
-    }
-    CLV_HIP(hipMemsetAsync(s->d_ticket, 0, sizeof(uint32_t), s->stream));
-    CLV_HIP(hipMemsetAsync(s->d_done, 0, sizeof(uint32_t) * (size_t)ntask, s->stream));
-    CLV_HIP(hipMemsetAsync(s->d_arrive, 0, sizeof(uint32_t) * n_arrive, s->stream));
-    CLV_HIP(hipMemcpyAsync(s->d_lam_alt, s->d_lam, nl, hipMemcpyDeviceToDevice, s->stream));
-    CLV_HIP(hipMemcpyAsync(s->d_mu_alt, s->d_mu, nl, hipMemcpyDeviceToDevice, s->stream));
-    if (s->d_sums_prev) CLV_HIP(hipMemcpyAsync(s->d_sums_prev, s->d_sums, sums_bytes, hipMemcpyDeviceToDevice, s->stream));
-    SweepArgs a = sweep_args(s, 0, 1);
-    a.hyper_out = s->d_hyper_alt;
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (s->timing) {
-      int rc = ensure_events(s);
-      if (rc) return rc;
-      e0 = s->ev[4 * s->ev_used];
-      e1 = s->ev[4 * s->ev_used + 1];
-      if (s->ev_sweeps.size() < TIMING_EVENTS) s->ev_sweeps.assign(TIMING_EVENTS, 1);
-      s->ev_sweeps[s->ev_used] = n;
-      CLV_HIP(hipEventRecord(e0, s->stream));
-    }
-    CLV_HIP(launch_stride(a, s->sweeps_done + 1, n, s->stride_grid, s->stream));
-    if (e1) CLV_HIP(hipEventRecord(e1, s->stream));
-    CLV_HIP(hipStreamSynchronize(s->stream));
-    if (__atomic_load_n(s->h_abort, __ATOMIC_ACQUIRE)) {
-      *s->h_abort = 0;
-      CLV_HIP(hipMemcpy(s->d_lam, s->d_lam_alt, nl, hipMemcpyDeviceToDevice));
-      CLV_HIP(hipMemcpy(s->d_mu, s->d_mu_alt, nl, hipMemcpyDeviceToDevice));
-      if (s->d_sums_prev) CLV_HIP(hipMemcpy(s->d_sums, s->d_sums_prev, sums_bytes, hipMemcpyDeviceToDevice));
-      Ctrl c{};
-      c.cur = s->sweeps_done;
-      CLV_HIP(hipMemcpy(s->d_ctrl, &c, sizeof(Ctrl), hipMemcpyHostToDevice));
-      s->slots_dirty = true;
-      if (s->timing) s->ev_used = 0;
-      return fail(CLV_EHIP, "stride sweep kernel: a wait timed out (not all workgroups resident?); state unchanged");
-    }
-    std::swap(s->d_hyper, s->d_hyper_alt);
-    if (s->graph_exec) {  // captured with the previous state pointers
-      CLV_HIP(hipGraphExecDestroy(s->graph_exec));
-      s->graph_exec = nullptr;
-    }
-    CLV_HIP(hipMemsetAsync(s->d_arrive, 0, sizeof(uint32_t) * n_arrive, s->stream));  // (the fused tail's invariant)
-    s->sweeps_done += n;
-    n_sweeps -= n;
-    if (s->timing && ++s->ev_used == TIMING_EVENTS) {
-      int rc = harvest_timing(s);
-      if (rc) return rc;
-    }
-  }
-  return CLV_OK;
-}
-
 // n launches of the fused sweep kernel (world size 1, or sharded with the fused peer exchange):
 // hipGraph chunks, or (timing) one event pair per launch.  Not waited for.
 int enqueue_fused_sweeps(clv_sampler* s, int64_t n_sweeps) {
@@ -1201,7 +1094,6 @@ int clv_run(clv_sampler* s, int64_t n_sweeps) {
     s->pending_init_hyper = false;
   }
   if (s->persistent) return run_persistent(s, n_sweeps);
-  if (s->stride_grid > 0) return run_stride(s, n_sweeps);
   rc = enqueue_fused_sweeps(s, n_sweeps);
   if (rc) return rc;
   CLV_HIP(hipStreamSynchronize(s->stream));

@@ -87,42 +87,6 @@ __device__ constexpr double EXP2_TAB[EXP_TAB_N] = {
     0x1.fa7c1819e90d8p+0, 0x1.fbdba3692d514p+0, 0x1.fd3c22b8f71f1p+0, 0x1.fe9d96b2a23d9p+0,
 };
 
-// (A/B, CLV_EXP32=1) a 32-entry table, 2^(j/32) = EXP2_TAB[8 j], stored compactly in the first 32
-// LDS slots — one 256-byte LDS row, so a wavefront's data-dependent gathers cannot conflict on a
-// bank — with r = x - k ln2/32, |r| <= ln2/64, and a degree-6 expm1 polynomial (2 more fma).
-#ifndef CLV_EXP32
-#define CLV_EXP32 0
-#endif
-#if CLV_EXP32
-__device__ __forceinline__ double exp32_core(double x, double tab, int ki) {
-  const double k = __builtin_fma(x, EXP_INV_L * 0.125, EXP_SHIFTER) - EXP_SHIFTER;
-  double r = __builtin_fma(-k, EXP_L_HI * 8.0, x);
-  r = __builtin_fma(-k, EXP_L_LO * 8.0, r);
-  double p = __builtin_fma(r, 1.0 / 720.0, 1.0 / 120.0);
-  p = __builtin_fma(p, r, 1.0 / 24.0);
-  p = __builtin_fma(p, r, 1.0 / 6.0);
-  p = __builtin_fma(p, r, 0.5);
-  p = __builtin_fma(p, r, 1.0);
-  p = p * r;
-  return __builtin_ldexp(__builtin_fma(tab, p, tab), ki >> 5);
-}
-__device__ __forceinline__ double exp_fast(double x, const double* lds_tab) {
-  const double t = __builtin_fma(x, EXP_INV_L * 0.125, EXP_SHIFTER);
-  const int ki = (int)(uint32_t)__builtin_bit_cast(uint64_t, t);
-  return exp32_core(x, lds_tab[ki & 31], ki);
-}
-__device__ __forceinline__ void exp_fast2(double x1, double x2, const double* lds_tab, double& e1, double& e2) {
-  const double t1 = __builtin_fma(x1, EXP_INV_L * 0.125, EXP_SHIFTER);
-  const double t2 = __builtin_fma(x2, EXP_INV_L * 0.125, EXP_SHIFTER);
-  const int ki1 = (int)(uint32_t)__builtin_bit_cast(uint64_t, t1);
-  const int ki2 = (int)(uint32_t)__builtin_bit_cast(uint64_t, t2);
-  const double tab1 = lds_tab[ki1 & 31];
-  const double tab2 = lds_tab[ki2 & 31];
-  e1 = exp32_core(x1, tab1, ki1);
-  e2 = exp32_core(x2, tab2, ki2);
-}
-__device__ __forceinline__ double exp_tab_entry(int j) { return EXP2_TAB[(j & 31) * 8]; }
-#else
 __device__ __forceinline__ double exp_tab_entry(int j) { return EXP2_TAB[j]; }
 __device__ __forceinline__ double exp_fast(double x, const double* lds_tab) {
   const double t = __builtin_fma(x, EXP_INV_L, EXP_SHIFTER);
@@ -163,7 +127,6 @@ __device__ __forceinline__ void exp_fast2(double x1, double x2, const double* ld
   e1 = __builtin_ldexp(__builtin_fma(tab1, p1, tab1), ki1 >> 8);
   e2 = __builtin_ldexp(__builtin_fma(tab2, p2, tab2), ki2 >> 8);
 }
-#endif  // CLV_EXP32
 
 // ---- Fast fp64 log for x > 0 normal (the sampler's Philox-mode logs: lambda, mu, the dropout
 // time's uniform or truncated-exponential argument, eta's Box-Muller radius).  ocml's log is ~95

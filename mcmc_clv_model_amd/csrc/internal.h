@@ -95,9 +95,6 @@ struct clv_sampler {
                                     // launch leaves them empty; only an aborted one does not)
   int64_t last_persist_n = 0;       // sweeps of the last persistent launch (rollback), 0 = none
   bool persistent = false;          // clv_run uses persist_kernel (all workgroups resident)
-  int stride_grid = 0;              // > 0: clv_run uses stride_kernel on this many resident workgroups
-  uint32_t* d_ticket = nullptr;     // stride kernel: the launch's ticket counter
-  uint32_t* d_done = nullptr;       // stride kernel: [chain][block] sweeps of the launch whose state is final
   int persist_bpc = 0, n_cu = 0;    // persist_kernel occupancy (workgroups per CU), CUs
   // world size > 1: persistent kernel with the peer (xGMI) exchange
   bool p2p_capable = false;         // the grid fits at once and the unit partials fit UMAIL
@@ -133,7 +130,6 @@ struct clv_sampler {
   int64_t inflight_n = 0;           // sweeps of the persistent launch in flight (persist_launch)
   hipEvent_t inflight_done = nullptr;  // its end event (null: wait with hipStreamSynchronize)
   int pre_variates = 1;             // CLV_PRE_VARIATES (read at create)
-  int prio_mh = 0;                  // CLV_PRIO_MH (read at create): persistent kernel MH-phase priority
   bool timing_record = true;        // timed persistent launches bracketed by hipEventRecord
                                     // (CLV_TIMING_RECORD=0: the dispatch's own timestamps)
 

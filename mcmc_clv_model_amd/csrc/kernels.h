@@ -115,7 +115,6 @@ struct SweepArgs {
   int rank;
   const int32_t* wg_map;     // persistent kernel: linear workgroup -> (chain << 16 | block), or null
   int pre_variates;          // persistent kernel: draw the next sweep's MH variates during the hand-off
-  int prio_mh;               // persistent kernel: wave priority (s_setprio) of the MH phase, 0 = off
   // persistent kernel, world size 1: MH-variate producers / consumers (SIMD balancing, capi.hip
   // pc_plan).  pc_desc[linear workgroup][PC_DESC]: [0] chunks of its own next-sweep MH variates
   // this workgroup reads from vbuf instead of drawing them (consumer), [1] number of chunk tasks
@@ -123,11 +122,6 @@ struct SweepArgs {
   // vbuf: [2 (sweep parity)][linear workgroup][PRE_CHUNKS][PC_WORDS][BLOCK] packed float pairs.
   const int32_t* pc_desc;
   double* vbuf;
-  // stride kernel (world size 1, grids too large to be resident): ticket counter of the launch's
-  // (sweep, chain, block) tasks and, per (chain, block), the number of this launch's sweeps whose
-  // state is final (both zeroed by the host before each launch)
-  uint32_t* ticket;
-  uint32_t* done;
   // persistent kernel: the carried state at the end of a launch goes to these (the host swaps them
   // with lam / mu / hyper only if no wave aborted), the bound on every wait (s_memrealtime ticks,
   // 100 MHz) and a host-mapped copy of ctrl->abort (read by the host after the launch, no D2H copy)
@@ -154,9 +148,6 @@ hipError_t launch_group(const GroupArgs& a, hipStream_t st);
 hipError_t launch_persist(const SweepArgs& a, int64_t s_first, int64_t n_sweeps, hipStream_t st,
                           hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 hipError_t persist_occupancy(int D, int K, bool p2p, int* blocks_per_cu);
-hipError_t launch_stride(const SweepArgs& a, int64_t s_first, int64_t n_sweeps, int grid, hipStream_t st,
-                         hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
-hipError_t stride_occupancy(int D, int K, int* blocks_per_cu);
 hipError_t launch_hyper(const HyperArgs& a, bool replay, hipStream_t st);
 hipError_t launch_set_hyper(int D, int K, int n_chains, double* hyper, const double* beta_sigma,
                             double omega2, hipStream_t st);

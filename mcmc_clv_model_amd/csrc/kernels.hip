@@ -17,12 +17,6 @@
 #include "kernels.h"
 #include "philox.h"
 
-#ifndef CLV_MH_MASKED
-#define CLV_MH_MASKED 1  // MH accept as exec-masked 64-bit moves (mh_step)
-#endif
-#ifndef CLV_MH_THR_ASM
-#define CLV_MH_THR_ASM 0  // (A/B) MH accept threshold as a three-address v_fma_f64: c2 10.65 without, 10.68 with — off
-#endif
 #ifndef SWEEP_MH_PIPELINE
 #define SWEEP_MH_PIPELINE 1  // 1: next MH chunk's variates drawn during the current chunk's steps
 #endif
@@ -1041,9 +1035,7 @@ struct Cust {
 
 // Phase A1: the customer's loads (CBS row, covariates, state), issued before the workgroup's
 // exp-table barrier so their latency overlaps it.
-// WT: the state (lambda, mu) with write-through-coherent loads (the stride kernel: another
-// workgroup, possibly on another XCD, stored it during this launch).
-template <int D, int K, bool CL, bool WT = false>
+template <int D, int K, bool CL>
 __device__ __forceinline__ void cust_load(Cust<D, K, CL>& u, const SweepArgs& a, int c) {
   const Geometry& g = a.g;
   const int64_t i = u.i;
@@ -1058,13 +1050,8 @@ __device__ __forceinline__ void cust_load(Cust<D, K, CL>& u, const SweepArgs& a,
     for (int k = 1; k < K; ++k) u.xr_[k] = a.cov[(int64_t)(k - 1) * g.n + i];
   }
   const int64_t ci = (int64_t)c * g.n + i;
-  if constexpr (WT) {
-    u.lam = ld_wt(a.lam + ci);
-    u.mu = ld_wt(a.mu + ci);
-  } else {
-    u.lam = a.lam[ci];
-    u.mu = a.mu[ci];
-  }
+  u.lam = a.lam[ci];
+  u.mu = a.mu[ci];
   u.xi = a.x[i];
   u.gi = (uint32_t)(g.shard_begin + i);
 }
@@ -1218,19 +1205,10 @@ __device__ __forceinline__ double prop_lm(double a, double b, double c) {
 template <int D, int K, bool CL>
 __device__ __forceinline__ void mh_step(Cust<D, K, CL>& u, double s00, double s11, float t_l, float t_m, float l2u,
                                         const double* exp_tab) {
-#if CLV_MH_THR_ASM
-  // cur + ln2 log2 u as a three-address v_fma_f64 (the compiler's v_fmac form needed a v_mov_b64
-  // copy of cur every step); ln 2 from SGPRs
-  double thr;
-  const double ln2 = 0x1.62e42fefa39efp-1;
-  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(thr) : "v"((double)l2u), "s"(ln2), "v"(u.cur));
-#else
   const double thr = __builtin_fma((double)l2u, 0x1.62e42fefa39efp-1, u.cur);  // cur + ln2 log2 u
-#endif
   const double pl = clip70_fma(s00, (double)t_l, u.ll);
   const double pm = prop_lm(s11, (double)t_m, u.lm);
   const double plp = log_post_fast(u.fc, pl, pm, exp_tab);
-#if CLV_MH_MASKED
   // The accept as three exec-masked 64-bit moves (3 VALU) instead of six v_cndmask_b32 halves:
   // exec narrowed to the accepting lanes for the moves and restored inside the one asm block (so
   // still no branch: the chunk's steps stay one basic block).  Same predicate as below: 5 >= pm
@@ -1249,13 +1227,6 @@ __device__ __forceinline__ void mh_step(Cust<D, K, CL>& u, double s00, double s1
       : [ll] "+v"(u.ll), [lm] "+v"(u.lm), [cur] "+v"(u.cur), [m0] "=&s"(m0), [m1] "=&s"(m1), [sv] "=&s"(sv)
       : [pl] "v"(pl), [pm] "v"(pm), [plp] "v"(plp), [thr] "v"(thr), [five] "s"(five)
       : "scc");
-#else
-  // selects, not a branch: keeps a chunk's steps in one basic block with the next chunk's variates
-  const bool acc = (pm <= 5.0) & (plp > thr);
-  u.ll = acc ? pl : u.ll;
-  u.lm = acc ? pm : u.lm;
-  u.cur = acc ? plp : u.cur;
-#endif
 }
 
 // The sweep's S Philox-mode MH steps.  Software pipeline: the Philox blocks and t3 transforms of
@@ -1273,7 +1244,7 @@ __device__ __forceinline__ void mh_run(Cust<D, K, CL>& cu, const SlotPhilox& ph,
   float tl[MC], tm[MC], lu[MC];
   // trivariate launch-per-sweep instances (c5): the packed t3 pair — c5 122.8 -> 121.6 us per sweep,
   // bitwise the same variates (the persistent kernels keep the scalar form: c2 measured slower)
-  constexpr bool PK = D == 3 || CLV_T3_PACKED != 0;
+  constexpr bool PK = D == 3;
   if constexpr (!PIPE) {
   // no software pipeline (occupancy hides the latency instead): variates, then the chunk's steps
   for (int ch = q0; ch < n_chunks; ++ch) {
@@ -1464,9 +1435,7 @@ __device__ __forceinline__ CustOut<D> cust_finish(Cust<D, K, CL>& u, const Sweep
 
 // Phase C2: storage (bi:402-412, tri:539-571) — issued after the workgroup's partial has been
 // handed off, so the hand-off's store drain does not wait for them — and the carried state.
-// WT: state and running sums with write-through stores (and coherent loads of the sums): the
-// stride kernel's next sweep of this block may run on another XCD.
-template <int D, int K, bool CL, bool WT = false>
+template <int D, int K, bool CL>
 __device__ __forceinline__ void cust_store(const Cust<D, K, CL>& u, const CustOut<D>& o, const SweepArgs& a, int c,
                                            int64_t s, bool stored, bool store_state) {
   const Geometry& g = a.g;
@@ -1483,10 +1452,7 @@ __device__ __forceinline__ void cust_store(const Cust<D, K, CL>& u, const CustOu
     }
     if (a.sums) {
       double* sm = a.sums + (int64_t)c * CLV_N_SUM_STATS * g.n + i;
-      auto acc = [&](int k, double v) {
-        if constexpr (WT) st_wt(sm + k * g.n, ld_wt(sm + k * g.n) + v);
-        else sm[k * g.n] += v;
-      };
+      auto acc = [&](int k, double v) { sm[k * g.n] += v; };
       acc(CLV_SUM_LAMBDA, o.lam);
       acc(CLV_SUM_MU, o.mu);
       acc(CLV_SUM_Z, u.z ? 1.0 : 0.0);
@@ -1506,13 +1472,8 @@ __device__ __forceinline__ void cust_store(const Cust<D, K, CL>& u, const CustOu
   }
   if (store_state) {
     const int64_t ci = (int64_t)c * g.n + i;
-    if constexpr (WT) {
-      st_wt(a.lam + ci, o.lam);
-      st_wt(a.mu + ci, o.mu);
-    } else {
-      a.lam[ci] = o.lam;
-      a.mu[ci] = o.mu;
-    }
+    a.lam[ci] = o.lam;
+    a.mu[ci] = o.mu;
   }
 }
 
@@ -2247,14 +2208,6 @@ __device__ __forceinline__ const SweepArgs& loop_args(const SweepArgs& a) {
   else return a;
 }
 
-// Wave priority (s_setprio) for the persistent kernel's MH-phase experiment (SweepArgs::prio_mh).
-__device__ __forceinline__ void set_prio(int p) {
-  if (p == 3) __builtin_amdgcn_s_setprio(3);
-  else if (p == 2) __builtin_amdgcn_s_setprio(2);
-  else if (p == 1) __builtin_amdgcn_s_setprio(1);
-  else __builtin_amdgcn_s_setprio(0);
-}
-
 // P2P: world size > 1 with the peer exchange (a separate instance, so that the world-size-1
 // kernel carries none of its registers or LDS).
 template <int D, int K, bool P2P>
@@ -2296,7 +2249,6 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
   if (tid == 0) s_abort = 0;
 
   if (b == g.nb_local) {  // the chain's level-2 workgroup
-    if (a.prio_mh) set_prio(3);  // (experiment) the draw is on every chain's critical path
     persist_level2<D, K, P2P>(a, s_first, n_sweeps, c, k0, k1, wgi, it_stamp, (double*)pool);
     return;
   }
@@ -2359,7 +2311,6 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
       if (s_abort) return;
     }
     CLV_P_STAMP(a.stamps, wgi, 1, stp);
-    if (a.prio_mh) set_prio(a.prio_mh);  // (experiment) MH phase ahead of a co-resident wave's variates
     StatGen<D, K> st{};
     CustOut<D> out{};
     if (cu.active) {
@@ -2388,7 +2339,6 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
     }
 #endif
     if (tid < NS) st_wt(parts + (int64_t)b * NS + tid, tot[tid]);  // one contiguous 8*NS-byte record
-    if (a.prio_mh) set_prio(0);
     CLV_P_STAMP(a.stamps, wgi, 5, stp);
     CLV_P_STAMP(a.stamps, wgi, 8, stp);
     CLV_P_STAMP(a.stamps, wgi, 9, stp);
@@ -2417,307 +2367,6 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
     a.lam_out[ci] = cu.lam;
     a.mu_out[ci] = cu.mu;
   }
-}
-
-// ---------------------------------------------------------------------------------------------
-// Stride kernel (world size 1, Philox mode, grids too large to be resident at once: c4, c5).
-// One launch runs n_sweeps sweeps on a resident grid of G workgroups that take (sweep, chain,
-// block) tasks from a ticket counter in order, one at a time, with the state in HBM:
-//   wait until the block's previous sweep is final (its `done` count) -> loads, z / tau (state
-//   only) -> [the chain's (beta, Sigma) of this sweep not published yet: draw the first MH
-//   variate chunks ahead into LDS, then wait] -> MH, finish, the block partial (write-through),
-//   state / draws / running sums (write-through) -> `done` -> the fused path's two-level arrival:
-//   the unit's last block sums the unit, the chain's last unit reduces every unit partial in the
-//   fixed order and draws (beta, Sigma) of the next sweep, published into a sweep-parity slot set
-//   with the sweep as a tag (hyp2[.][H_TAG]), the next draw's variates come from the chain's last
-//   block (hvar, by sweep parity).
-// So the level-2 draw of sweep s no longer idles the GPU: the other workgroups already load and
-// prepare their first task of sweep s + 1, and there are no kernel boundaries between sweeps.
-// Sums are formed exactly as in the fused path (same partials, same orders): results are bitwise
-// those of the launch-per-sweep kernel.  Progress: a workgroup holds one task at a time and the
-// holder of the oldest unfinished task waits only on older sweeps, so with every workgroup
-// resident nothing waits forever; every wait is bounded anyway (wait_ticks), a timed-out wave
-// raises ctrl->abort and the host restores the state the launch started from.  Counters are
-// monotonic within a launch (the unit's last block of sweep it sees (it + 1) * blocks - 1).
-// ---------------------------------------------------------------------------------------------
-#ifndef CLV_STRIDE_PRE
-#define CLV_STRIDE_PRE(D) ((D) == 2 ? 2 : 0)
-#endif
-#ifndef CLV_STRIDE_FRESH_ARGS
-#define CLV_STRIDE_FRESH_ARGS 1
-#endif
-#ifndef CLV_STRIDE_PIPE
-#define CLV_STRIDE_PIPE 0  // (4 waves per SIMD hide the MH chain's latency; the pipeline's registers spilled)
-#endif
-template <int D, int K>
-struct StridePre {  // MH-variate chunks drawn ahead while (beta, Sigma) are awaited (LDS: 12 KiB each)
-  static constexpr int value = CLV_STRIDE_PRE(D);
-};
-
-// Lane l of one wavefront: the level-2 draw's Philox variate of record slot l (hyper_variates'
-// layout of the fused path's hvar: [0, 3) inverse-Wishart normals, [3, 6) chi-squares, [8, 8 + DK)
-// beta normals), 0 elsewhere.
-template <int D, int K>
-__device__ __noinline__ double stride_hyper_variate(const SweepArgs& a, uint32_t k0, uint32_t k1, int64_t hs, int l) {
-  if (l < D * (D - 1) / 2) return hyper_normal(k0, k1, HSLOT_NORMAL0 + l, (uint32_t)hs);
-  if (l >= 3 && l < 3 + D) return chi2_draw(k0, k1, (uint32_t)hs, l - 3, a.h.nu_n - D + 1 + (l - 3));
-  if (l >= 8 && l < 8 + D * K) return hyper_normal(k0, k1, HSLOT_BETA_NORMAL0 + (l - 8), (uint32_t)hs);
-  return 0.0;
-}
-
-template <int D, int K>
-__device__ __forceinline__ void stride_body(const SweepArgs& a0, int64_t s_first, int64_t n_sweeps) {
-  const SweepArgs& a = a0;
-  constexpr int NT = BLOCK;
-  constexpr int NXY = K * D;
-  constexpr int NYY = D * (D + 1) / 2;
-  constexpr int NS = NXY + NYY + 1;
-  constexpr bool CL = CovLds<D, K>::value;
-  constexpr int NPRE = StridePre<D, K>::value;
-  constexpr int POOL = NPRE > 0 ? NPRE * MH_CHUNK_STEPS * BLOCK * 12 : 16;
-  __shared__ double red[BLOCK / 64][NS];
-  __shared__ double tot[NS];
-  __shared__ __attribute__((aligned(16))) double exp_tab[D == 3 ? FAST_TAB_N3 : FAST_TAB_N];
-  __shared__ double Hs[HS];
-  __shared__ double cov_s[CL ? (K - 1) * BLOCK : 1];
-  __shared__ __attribute__((aligned(16))) char pool[POOL];
-  __shared__ double var_iw[4], var_chi[4], var_noise[32];
-  __shared__ L2Scratch l2;
-  __shared__ uint32_t s_tk, s_last, s_abort, s_ready;
-  __shared__ int64_t s_hkey;  // it * n_chains + c of the (beta, Sigma) held in Hs, -1 = none
-  const int tid0 = threadIdx.x;
-  fast_tab_fill(exp_tab, tid0, BLOCK, D == 3);
-  stage_prior(a.h.V, &l2);  // any workgroup may draw a chain's level 2
-  if (tid0 == 0) {
-    s_abort = 0;
-    s_hkey = -1;
-  }
-  __syncthreads();
-  for (;;) {
-#if CLV_STRIDE_FRESH_ARGS
-    const SweepArgs& a = kernargs_fresh();
-#endif
-    // per-lane values recomputed every task from an opaque lane index (held across the loop they
-    // were hoisted, kept live and spilled)
-    int tid = tid0;
-    asm volatile("" : "+v"(tid));
-    const Geometry& g = a.g;
-    const int64_t nb = g.nb_local;
-    const int64_t ntask = (int64_t)g.n_chains * nb;  // tasks per sweep
-    const int64_t total = n_sweeps * ntask;
-    const int bpu = g.blocks_per_unit;
-    const int64_t n_units = (nb + bpu - 1) / bpu;  // units of a chain in this launch
-    const PreVariates pv{(float2*)pool, (float*)(pool + NPRE * MH_CHUNK_STEPS * BLOCK * 8), tid};
-    if (tid == 0) s_tk = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    const uint32_t k = __builtin_amdgcn_readfirstlane(s_tk);  // (the host keeps total + grid < 2^32)
-    if ((int64_t)k >= total || s_abort) break;
-    const uint32_t it32 = k / (uint32_t)ntask;
-    const uint32_t rr = k - it32 * (uint32_t)ntask;
-    const int c = (int)(rr / (uint32_t)nb);
-    const int b = (int)(rr - (uint32_t)c * (uint32_t)nb);
-    const int64_t it = it32;
-    const int64_t s = uniform64(s_first + it);
-    const int64_t cb = (int64_t)c * nb + b;
-    // (1) this block's state of sweep s - 1 is final (its task of the previous sweep counted it)
-    if (it > 0 && tid < 64) {
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      for (uint32_t poll = 0;; ++poll) {
-        const uint32_t d = __hip_atomic_load(a.done + cb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (d >= (uint32_t)it) break;
-        if (wait_expired(a, t0, poll)) {
-          if (tid == 0) s_abort = 1;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-    }
-    __syncthreads();
-    if (s_abort) break;
-    // (2) loads, z / tau
-    Cust<D, K, CL> cu;
-    cu.cl = cov_s + tid;
-    {
-      const int64_t i = (int64_t)b * BLOCK + tid;
-      cu.active = i < g.n;
-      cu.i = cu.active ? i : (g.n > 0 ? g.n - 1 : 0);
-    }
-    cust_load<D, K, CL, true>(cu, a, c);
-    uint32_t k0, k1;
-    chain_key(a.r.seed, (int64_t)a.r.chain_first + c, &k0, &k1);
-    if (cu.active) cust_ztau<D, K, false>(cu, a, s, k0, k1, nullptr, exp_tab);
-    // (3) (beta, Sigma) of sweep s for chain c (LDS copy kept while the workgroup's tasks stay in
-    //     (sweep, chain)); if not published yet, draw the first MH chunks ahead, then wait
-    int npre = 0;
-    const int64_t key = it * g.n_chains + c;
-    if (s_hkey != key) {
-      const double* src = a.hyp2 + ((int64_t)(s & 1) * g.n_chains + c) * HS;
-      if (tid < 64) {
-        if (it == 0) {  // from before this launch
-          Hs[tid] = a.hyper[(int64_t)c * HS + tid];
-          if (tid == 0) s_ready = 1;
-        } else {
-          const double v = ld_wt(src + tid);
-          const bool ok = __all(slot_full(v)) && __shfl(v, H_TAG, 64) == (double)s;  // the sweep tag
-          if (ok) Hs[tid] = v;
-          if (tid == 0) s_ready = ok ? 1u : 0u;
-        }
-      }
-      __syncthreads();
-      if (!s_ready) {
-        if constexpr (NPRE > 0) {
-          if (cu.active) mh_pre_variates<NPRE>(SlotPhilox(k0, k1, cu.gi, (uint32_t)s), g.S, pv);
-          npre = NPRE;
-        }
-        if (tid < 64) {
-          const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-          for (uint32_t poll = 0;; ++poll) {
-            const double v = ld_wt(src + tid);
-            const double tag = __shfl(v, H_TAG, 64);
-            if (__all(slot_full(v)) && tag == (double)s) {
-              Hs[tid] = v;
-              break;
-            }
-            if (wait_expired(a, t0, poll)) {
-              if (tid == 0) s_abort = 1;
-              break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-          }
-        }
-      }
-      if (tid == 0) s_hkey = key;
-      __syncthreads();
-      if (s_abort) break;
-    }
-    // (4) MH, finish, block partial, state
-    StatGen<D, K> st{};
-    CustOut<D> out{};
-    const bool stored = is_stored(s, g);
-    if (cu.active) {
-      cust_coeffs<D, K, false>(cu, Hs, exp_tab);
-      const double s00 = Hs[H_S00];
-      const double s11 = Hs[H_S11];
-      const SlotPhilox ph(k0, k1, cu.gi, (uint32_t)s);
-      if constexpr (NPRE > 0) {
-        if (npre > 0) mh_run_pre<NPRE>(cu, pv, s00, s11, g.S, exp_tab);
-      }
-      mh_run<CLV_STRIDE_PIPE != 0>(cu, ph, s00, s11, g.S, exp_tab, npre);
-      out = cust_finish<D, K, false>(cu, a, s, stored, Hs, k0, k1, nullptr, exp_tab, st);
-    }
-    block_reduce_gen<NS, SWEEP_REDUCE_CHUNK>(st, red, tot);
-    if (tid < NS) st_wt(a.blockpart + ((int64_t)c * g.stride + tid) * g.blocks_per_rank + b, tot[tid]);
-    if (cu.active) cust_store<D, K, CL, true>(cu, out, a, c, s, stored, true);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // partial, state, sums landed (each wave its own)
-    __syncthreads();
-    if (tid == 0) __hip_atomic_store(a.done + cb, (uint32_t)(it + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // (5) arrivals: the unit's last block forms the unit partial (group_kernel's order)
-    const double* units = a.blockpart;
-    if (bpu > 1) {
-      const int u = b / bpu;
-      const int nbu = (int)min((int64_t)bpu, nb - (int64_t)u * bpu);
-      if (tid == 0) {
-        uint32_t* ctr = a.unit_arrive + (int64_t)c * g.units_per_rank + u;
-        const uint32_t old = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_last = old == (uint32_t)((it + 1) * nbu - 1) ? 1u : 0u;
-      }
-      __syncthreads();
-      if (s_last) {
-        if (tid < NS) {
-          const double* p = a.blockpart + ((int64_t)c * g.stride + tid) * g.blocks_per_rank + (int64_t)u * bpu;
-          double t = 0.0;
-          int bb = 0;
-          for (; bb + 8 <= bpu; bb += 8) {
-            double v[8];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) v[q] = ld_wt(p + bb + q);
-#pragma unroll
-            for (int q = 0; q < 8; ++q) t += v[q];
-          }
-          for (; bb < bpu; ++bb) t += ld_wt(p + bb);
-          st_wt(a.unitpart + ((int64_t)c * g.stride + tid) * g.units_per_rank + u, t);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      __syncthreads();
-      if (!s_last) continue;
-      units = a.unitpart;
-    }
-    if (tid == 0) {
-      const uint32_t old = __hip_atomic_fetch_add(a.chain_arrive + c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_last = old == (uint32_t)((it + 1) * n_units - 1) ? 1u : 0u;
-    }
-    __syncthreads();
-    if (!s_last) continue;
-    // (6) the chain's last unit: fixed-order sum of every unit partial, the level-2 draw, the
-    //     next sweep's (beta, Sigma) published (or carried out of the launch after its last sweep)
-    const int64_t hs = (D == 2) ? s + 1 : s;
-    if (tid < 64) {  // this draw's variates: drawn after the previous draw of the chain (tagged), else here
-      const double* hv = a.hvar_out + ((int64_t)(s & 1) * g.n_chains + c) * HV;
-      const double v = ld_wt(hv + tid % HV);
-      const bool have = __shfl(v, HV - 1, 64) == (double)hs;
-      double w = v;
-      if (!have) w = stride_hyper_variate<D, K>(a, k0, k1, hs, tid);
-      if (tid < 3) var_iw[tid] = w;
-      else if (tid < 6) var_chi[tid - 3] = w;
-      else if (tid >= 8 && tid < 8 + D * K) var_noise[tid - 8] = w;
-    }
-    double acc[NS];
-    hyper_sum_units<NS, NT>(a.h, c, units, acc);
-    block_reduce<NS, NT>(acc, red, tot);  // (its barriers publish the variates)
-    double* hyp_c = a.hyp2 + (int64_t)c * HS;
-    if (it > 0 && tid < HS) st_wt(hyp_c + (int64_t)(s & 1) * g.n_chains * HS + tid, slot_empty());  // every reader of s has read it
-    level2_draw<D, K>(tot, var_iw, var_chi, var_noise, false, &l2);
-    if (tid < HS) Hs[tid] = 0.0;  // (wavefront 0: ordered before the finalisation's writes)
-    if (tid == 0) {
-      double Sig[D][D];
-#pragma unroll
-      for (int p = 0; p < D; ++p)
-#pragma unroll
-        for (int q = 0; q < D; ++q) Sig[p][q] = l2.Sig[p * D + q];
-      finalize_hyper<D, K, true>(l2.beta, Sig, a.h.omega2, Hs);
-      Hs[H_TAG] = (double)(s + 1);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the reset landed before the publish
-    __syncthreads();
-    const bool last = it == n_sweeps - 1;
-    if (tid < HS) {
-      if (last) a.hyper_out[(int64_t)c * HS + tid] = Hs[tid];
-      else st_wt(hyp_c + (int64_t)((s + 1) & 1) * g.n_chains * HS + tid, Hs[tid]);
-    }
-    const bool store_l2 = hs >= 1 && is_stored(hs, g);
-    double* o = store_l2 ? a.h.level2 + ((int64_t)c * g.n_draws + draw_index(hs, g)) * g.l2w : nullptr;
-    if (tid < K * D && store_l2) o[(tid % D) * K + tid / D] = l2.beta[tid];  // beta.T.ravel() (bi:411)
-    if (tid == 0) {
-      if (store_l2) {
-        int q = K * D;
-#pragma unroll
-        for (int p = 0; p < D; ++p)
-#pragma unroll
-          for (int r = p; r < D; ++r) o[q++] = l2.Sig[p * D + r];  // bi:412, tri:550-554
-      }
-      if (is_stored(s, g)) a.h.loglik[(int64_t)c * g.n_draws + draw_index(s, g)] = tot[NS - 1] / (double)g.n_global;
-      if (last) a.ctrl_rw->cur = s;
-      s_hkey = last ? -1 : key + g.n_chains;  // this workgroup holds (beta, Sigma) of (it + 1, c) already
-    }
-    if (!last && tid < 64) {  // the chain's next draw's variates, off its critical path; the tag last
-      double* hv = a.hvar_out + ((int64_t)((s + 1) & 1) * g.n_chains + c) * HV;
-      const double w = stride_hyper_variate<D, K>(a, k0, k1, hs + 1, tid);
-      if (tid < HV - 1) st_wt(hv + tid, w);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (tid == 0) st_wt(hv + HV - 1, (double)(hs + 1));
-    }
-    __syncthreads();
-  }
-}
-
-template <int D, int K>
-__global__ __launch_bounds__(BLOCK) void stride_kernel(SweepArgs a, int64_t s_first, int64_t n_sweeps) {
-  stride_body<D, K>(a, s_first, n_sweeps);
-}
-template <int D, int K>
-__global__ __launch_bounds__(BLOCK, 4) void stride_kernel_occ4(SweepArgs a, int64_t s_first, int64_t n_sweeps) {
-  stride_body<D, K>(a, s_first, n_sweeps);
 }
 
 // (beta, Sigma) -> hyper state for every chain: [chain][K*D + D*D] input.
@@ -2760,32 +2409,12 @@ __global__ void debug_variates_kernel(uint64_t seed, int chain, uint32_t sweep, 
   ea[i] = -log_fast(u53_open0(r.z, r.w), tab);  // as cust_ztau's alive dropout time
   ez[i] = eta_normal(k0, k1, (uint32_t)i, sweep, tab);
   const SlotPhilox ph(k0, k1, (uint32_t)i, sweep);
-#if CLV_MH_PACK
-  for (int q = 0; 4 * q < S; ++q) {  // the words of mh_chunk_variates (csrc/philox.h), uniforms exposed
-    uint32_t W[12];
-    for (int k = 0; k < 3; ++k) {
-      const u32x4 r = ph(SLOT_MH0 + 3u * (uint32_t)q + (uint32_t)k);
-      W[4 * k] = r.x;
-      W[4 * k + 1] = r.y;
-      W[4 * k + 2] = r.z;
-      W[4 * k + 3] = r.w;
-    }
-    for (int st = 0; st < 4 && 4 * q + st < S; ++st) {
-      const int64_t j = 4 * q + st;
-      const uint32_t a = W[3 * st], b = W[3 * st + 1], c = W[3 * st + 2];
-      tl[j * n + i] = t3_f32(uf24(a), angle12(a, (c >> 24) & 0xfu));
-      tm[j * n + i] = t3_f32(uf24(b), angle12(b, c >> 28));
-      ua[j * n + i] = uf24(c);
-    }
-  }
-#else
   for (int j = 0; j < S; ++j) {
     const u32x4 r = ph(SLOT_MH0 + (uint32_t)j);
     tl[(int64_t)j * n + i] = t3_f32(uf32(r.x), angle_hi(r.z));
     tm[(int64_t)j * n + i] = t3_f32(uf32(r.y), angle_lo(r.z));
     ua[(int64_t)j * n + i] = uf32(r.w);
   }
-#endif
 }
 
 // in: [V 81][cholV 81][A0B0 27][S0B 9] prior block, then xty(K*D) yty(D*D) iwn(3) chi2(3) z(D*K)
@@ -2919,43 +2548,6 @@ hipError_t launch_persist(const SweepArgs& a, int64_t s_first, int64_t n_sweeps,
   CLV_FOR_K(CLV_CASE, 3, false)
   CLV_FOR_K(CLV_CASE, 2, true)
   CLV_FOR_K(CLV_CASE, 3, true)
-#undef CLV_CASE
-  return hipErrorInvalidValue;
-}
-
-template <int D, int K>
-hipError_t launch_stride_t(const SweepArgs& a, int64_t s_first, int64_t n_sweeps, int grid, hipStream_t st,
-                           hipEvent_t e0, hipEvent_t e1) {
-  if constexpr (SweepOcc<D, K>::value >= 4) {
-    if (e0) hipExtLaunchKernelGGL((stride_kernel_occ4<D, K>), dim3(grid), dim3(BLOCK), 0, st, e0, e1, 0, a, s_first, n_sweeps);
-    else hipLaunchKernelGGL((stride_kernel_occ4<D, K>), dim3(grid), dim3(BLOCK), 0, st, a, s_first, n_sweeps);
-  } else {
-    if (e0) hipExtLaunchKernelGGL((stride_kernel<D, K>), dim3(grid), dim3(BLOCK), 0, st, e0, e1, 0, a, s_first, n_sweeps);
-    else hipLaunchKernelGGL((stride_kernel<D, K>), dim3(grid), dim3(BLOCK), 0, st, a, s_first, n_sweeps);
-  }
-  return hipGetLastError();
-}
-
-hipError_t launch_stride(const SweepArgs& a, int64_t s_first, int64_t n_sweeps, int grid, hipStream_t st,
-                         hipEvent_t e0, hipEvent_t e1) {
-#define CLV_CASE(DD, KK, RR) \
-  if (a.g.D == DD && a.g.K == KK) return launch_stride_t<DD, KK>(a, s_first, n_sweeps, grid, st, e0, e1);
-  CLV_FOR_K(CLV_CASE, 2, 0)
-  CLV_FOR_K(CLV_CASE, 3, 0)
-#undef CLV_CASE
-  return hipErrorInvalidValue;
-}
-
-hipError_t stride_occupancy(int D, int K, int* blocks_per_cu) {
-#define CLV_CASE(DD, KK, RR)                                                                                       \
-  if (D == DD && K == KK) {                                                                                        \
-    if constexpr (SweepOcc<DD, KK>::value >= 4)                                                                    \
-      return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, stride_kernel_occ4<DD, KK>, BLOCK, 0);    \
-    else                                                                                                           \
-      return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, stride_kernel<DD, KK>, BLOCK, 0);         \
-  }
-  CLV_FOR_K(CLV_CASE, 2, 0)
-  CLV_FOR_K(CLV_CASE, 3, 0)
 #undef CLV_CASE
   return hipErrorInvalidValue;
 }

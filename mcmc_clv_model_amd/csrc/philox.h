@@ -12,9 +12,6 @@
 
 
 #define CLV_HD __host__ __device__ __forceinline__
-#ifndef CLV_MH_ROUNDS
-#define CLV_MH_ROUNDS 10  // Philox4x32-10; other values only in cost-measurement builds (tools/)
-#endif
 
 namespace clv {
 
@@ -110,7 +107,7 @@ struct SlotPhilox {
       a1 += 0xBB67AE85u;
     }
 #pragma unroll
-    for (int r = 2; r < CLV_MH_ROUNDS; ++r) {  // (CLV_MH_ROUNDS: measurement builds only)
+    for (int r = 2; r < 10; ++r) {
       const uint64_t q0 = (uint64_t)0xD2511F53u * c.x;
       const uint64_t q1 = (uint64_t)0xCD9E8D57u * c.z;
       c = u32x4{xor3((uint32_t)(q1 >> 32), c.y, a0), (uint32_t)q1, xor3((uint32_t)(q0 >> 32), c.w, a1), (uint32_t)q0};
@@ -143,9 +140,6 @@ __device__ __forceinline__ float log2_f32(float u) {  // v_log_f32 (the MH step 
 // uniform u is a full 32-bit word; the angle v (revolutions, v_cos_f32) has 16-bit resolution —
 // a symmetric lattice of angles, so the proposal stays symmetric and MH stays exact.
 __device__ __forceinline__ float t3_f32(float u, float v) {
-#ifdef CLV_T3_CHEAP  // cost-measurement builds only: no transcendentals (not a t3 variate)
-  return (u - 0.5f) * v;
-#endif
   const float p = __builtin_amdgcn_exp2f(-(2.0f / 3.0f) * __builtin_amdgcn_logf(u));  // U^(-2/3)
   const float r = __builtin_amdgcn_sqrtf(__builtin_fmaf(3.0f, p, -3.0f));  // 3 (p - 1), one rounding
   return r * __builtin_amdgcn_cosf(v);
@@ -160,9 +154,9 @@ __device__ __forceinline__ float angle_lo(uint32_t w) { return (float)(w & 0xfff
 // with every non-transcendental operation on the PAIR in one packed fp32 instruction
 // (v_pk_fma_f32 / v_pk_mul_f32: two lanes' worth per issue): the same IEEE operations in the same
 // order as two t3_f32 calls, so the same bits, in 17 VALU instead of 21.
-#ifndef CLV_T3_PACKED
-#define CLV_T3_PACKED 0  // default of every call site but mh_run's trivariate instances: measured at c2
-#endif                   // 10.80 -> 10.87 us per sweep and c4 85.0 -> 87.2 (packed); c5 122.8 -> 121.6
+// Used by the trivariate launch-per-sweep instances only (c5 122.8 -> 121.6 us per sweep); the
+// bivariate and persistent kernels keep t3_f32 (measured slower with the pair: c2 10.80 -> 10.87,
+// c4 85.0 -> 87.2).
 #if defined(__clang__)  // (clang vector extension; the header is also host-compiled by g++ in tests)
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f32x2 t3_pair(uint32_t wl, uint32_t wm, uint32_t wz) {
@@ -181,9 +175,6 @@ __device__ __forceinline__ f32x2 t3_pair(uint32_t wl, uint32_t wm, uint32_t wz) 
   const f32x2 cs = {__builtin_amdgcn_cosf(ang.x), __builtin_amdgcn_cosf(ang.y)};
   return r * cs;
 }
-#else
-#undef CLV_T3_PACKED
-#define CLV_T3_PACKED 0
 #endif
 
 // Words of the MH steps: step j uses the four words of Philox block SLOT_MH0 + j:
@@ -191,53 +182,15 @@ __device__ __forceinline__ f32x2 t3_pair(uint32_t wl, uint32_t wm, uint32_t wz) 
 // w = accept uniform.  Chunk q = steps 4q .. 4q+3.
 constexpr int MH_CHUNK_STEPS = 4;
 
-#ifndef CLV_MH_PACK
-#define CLV_MH_PACK 0
-#endif
-#if CLV_MH_PACK
-// Four MH steps from THREE Philox blocks (chunk q: blocks SLOT_MH0 + 3q .. 3q + 2, twelve words
-// W0..W11).  Step i takes words a = W[3i], b = W[3i+1], c = W[3i+2]: 24-bit radius uniforms of t_l
-// (a) and t_m (b) and the 24-bit accept uniform (c) from the low 24 bits, (k + 1) 2^-24 in (0, 1];
-// the two 12-bit angles from the top bytes: t_l's = a[31:24] . c[27:24], t_m's = b[31:24] . c[31:28]
-// (revolutions).  96 bits per step instead of 128: a quarter fewer Philox blocks.
-constexpr int MH_BLOCKS_PER_CHUNK = 3;
-__device__ __forceinline__ float uf24(uint32_t w) {  // (k + 1) 2^-24, k = w[23:0]: exact in fp32
-  return __builtin_fmaf((float)(w & 0xffffffu), 0x1.0p-24f, 0x1.0p-24f);
-}
-__device__ __forceinline__ float angle12(uint32_t hi8_word, uint32_t lo4) {  // (hi8 . lo4) 2^-12
-  return __builtin_fmaf((float)(hi8_word >> 24), 0x1.0p-8f, (float)lo4 * 0x1.0p-12f);
-}
-template <bool PACKED = false, class PH>  // (PACKED: unused here)
-__device__ __forceinline__ void mh_chunk_variates(const PH& ph, uint32_t q, float (&t_l)[4], float (&t_m)[4],
-                                                  float (&log2_u)[4]) {
-  uint32_t W[12];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    const u32x4 r = ph(SLOT_MH0 + 3u * q + (uint32_t)k);
-    W[4 * k] = r.x;
-    W[4 * k + 1] = r.y;
-    W[4 * k + 2] = r.z;
-    W[4 * k + 3] = r.w;
-  }
-#pragma unroll
-  for (int i = 0; i < MH_CHUNK_STEPS; ++i) {
-    const uint32_t a = W[3 * i], b = W[3 * i + 1], c = W[3 * i + 2];
-    t_l[i] = t3_f32(uf24(a), angle12(a, (c >> 24) & 0xfu));
-    t_m[i] = t3_f32(uf24(b), angle12(b, c >> 28));
-    log2_u[i] = log2_f32(uf24(c));
-  }
-}
-#else
-constexpr int MH_BLOCKS_PER_CHUNK = 4;
 // One chunk's variates: t_l, t_m and log2(U_accept) of 4 consecutive MH steps.  PACKED: the pair
 // of t3 transforms as t3_pair (the same bits; the launch-per-sweep trivariate kernel takes it)
-template <bool PACKED = (CLV_T3_PACKED != 0), class PH>
+template <bool PACKED = false, class PH>
 __device__ __forceinline__ void mh_chunk_variates(const PH& ph, uint32_t q, float (&t_l)[4], float (&t_m)[4],
                                                   float (&log2_u)[4]) {
 #pragma unroll
   for (int i = 0; i < MH_CHUNK_STEPS; ++i) {
     const u32x4 r = ph(SLOT_MH0 + (uint32_t)MH_CHUNK_STEPS * q + (uint32_t)i);
-#if defined(__clang__) && !defined(CLV_T3_CHEAP)
+#if defined(__clang__)
     if constexpr (PACKED) {
       const f32x2 t = t3_pair(r.x, r.y, r.z);
       t_l[i] = t.x;
@@ -253,6 +206,5 @@ __device__ __forceinline__ void mh_chunk_variates(const PH& ph, uint32_t q, floa
     log2_u[i] = log2_f32(uf32(r.w));
   }
 }
-#endif
 
 }  // namespace clv

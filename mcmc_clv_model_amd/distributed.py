@@ -34,9 +34,50 @@ VERIFY_WAIT_MS = 500.0  # in-kernel wait bound while the peer exchange is checke
 
 
 def run_wait_ms() -> float:
-    """The wait bound afterwards: clv_create's default with peers (10 s) or CLV_WAIT_TIMEOUT_MS."""
+    """The wait bound afterwards: clv_create's default with peers (10 s) or CLV_WAIT_TIMEOUT_MS,
+    parsed as clv_create parses it (C atof: the longest numeric prefix, 0 if none; at least 1 ms),
+    so a value clv_create accepted never raises here."""
     import os
-    return float(os.environ.get("CLV_WAIT_TIMEOUT_MS", "10000"))
+    import re
+    v = os.environ.get("CLV_WAIT_TIMEOUT_MS")
+    if v is None:
+        return 10000.0
+    m = re.match(r"\s*[+-]?(\d+\.?\d*|\.\d+)([eE][+-]?\d+)?", v)
+    try:
+        ms = float(m.group(0)) if m else 0.0
+    except ValueError:
+        ms = 0.0
+    return max(1.0, ms) if ms == ms else 1.0
+
+
+def graph_sizes_all(chunk: int) -> list:
+    """The graph sizes a step may replay: ``chunk`` and every power of two below it."""
+    out, k = [int(chunk)], 1
+    while k < chunk:
+        out.append(k)
+        k *= 2
+    return sorted(set(out), reverse=True)
+
+
+def graph_sizes(n: int, chunk: int) -> list:
+    """Graph replays covering ``n`` sweeps: as many ``chunk``-sweep graphs as fit, then the binary
+    decomposition of the rest (a 20-sweep step with chunk 32 replays the 16- and 4-sweep graphs),
+    so no step of any length falls back to eager launches."""
+    out = []
+    if chunk <= 0:
+        return out
+    while n >= chunk:
+        out.append(int(chunk))
+        n -= chunk
+    k = 1
+    while k * 2 <= n:
+        k *= 2
+    while n > 0:
+        if n >= k:
+            out.append(k)
+            n -= k
+        k //= 2
+    return out
 
 
 def default_blocks_per_unit(n_global: int) -> int:
@@ -114,10 +155,11 @@ class _DeviceArray:
 class ShardedSampler:
     """This rank's shard of a problem on its GPU; sweeps with one all-gather per sweep.
 
-    ``graph_chunk`` > 0 captures that many sweeps (kernels, partial copy, RCCL all-gather) into a
-    torch.cuda.CUDAGraph on first use and replays it; the sweep index lives in device memory, so
-    one graph serves every chunk and the host issues one replay per chunk instead of ~5 calls per
-    sweep.
+    ``graph_chunk`` > 0: at the first step, that many sweeps (kernels, RCCL all-gather, level-2
+    kernel) and every power of two below it are captured into torch.cuda graphs; a step of n
+    sweeps replays ``graph_sizes(n, graph_chunk)`` of them (the sweep index lives in device memory,
+    so a graph serves any step) — one replay per chunk instead of ~5 host calls per sweep, for
+    steps of any length.
     """
 
     def __init__(self, p_global, *, rank: int, world: int, chains: int, mcmc: int, burnin: int, thin: int,
@@ -222,7 +264,10 @@ class ShardedSampler:
             except Exception as e:  # noqa: BLE001
                 same, err = False, e
             finally:
-                self.s.set_wait_timeout(run_wait_ms())
+                try:  # never mask the verification's outcome with an exception from the restore
+                    self.s.set_wait_timeout(run_wait_ms())
+                except Exception as e:  # noqa: BLE001
+                    err = err or e
             if not self._all_ok(same):
                 self.s.set_state(*snap, n0)  # the RCCL path carries on from the same state
                 if required:
@@ -264,16 +309,18 @@ class ShardedSampler:
             self.graph = None
         left = n
         if self.graph_chunk and not self.timing:
-            if self.graph is None and left >= self.graph_chunk:
-                self._capture()
-            while self.graph is not None and left >= self.graph_chunk:
+            if self.graph is None:  # every chunk size at the first such step (a warm-up step):
+                self.graph = {k: self._capture(k) for k in graph_sizes_all(self.graph_chunk)}
+            for k in graph_sizes(left, self.graph_chunk):
                 with torch.cuda.stream(self.stream):
-                    self.graph.replay()
-                self.s.note_sweeps(self.graph_chunk)
-                left -= self.graph_chunk
+                    self.graph[k].replay()
+                self.s.note_sweeps(k)
+                left -= k
         self._eager(left)
 
-    def _capture(self) -> None:
+    def _capture(self, k: int):
+        """k sweeps (sweep + group kernels, the all-gather, the level-2 kernel) captured into one
+        torch.cuda graph; the sweep index lives in device memory, so a graph serves any step."""
         torch = self.torch
         self.synchronize()
         g = torch.cuda.CUDAGraph()
@@ -282,13 +329,13 @@ class ShardedSampler:
             self.s.set_stream(cap.cuda_stream)
             self.cur = cap
             try:
-                self._eager(self.graph_chunk)
+                self._eager(k)
             finally:
                 self.cur = self.stream
         self.s.set_stream(self.base_stream)
-        self.s.note_sweeps(-self.graph_chunk)  # capture recorded the launches, it ran nothing
-        self.graph = g
+        self.s.note_sweeps(-k)  # capture recorded the launches, it ran nothing
         torch.cuda.synchronize()
+        return g
 
     def launch_info(self) -> dict:
         """clv_launch_info, with ``persistent`` = this rank runs whole steps in one launch (p2p with

@@ -13,6 +13,7 @@ Everything per sweep runs on the GPU (kernels.hip).
 from __future__ import annotations
 
 import ctypes
+import weakref
 import math
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence
@@ -183,6 +184,10 @@ class HipSampler:
 
     # ---- lifecycle
     def close(self) -> None:
+        """Destroy the handle.  A live HipGroup over this shard is closed first: clv_group_destroy
+        disconnects and synchronises its shards, so it must never run after a shard is gone."""
+        for grp in list(getattr(self, "_groups", ())):
+            grp.close()
         if getattr(self, "h", None):
             self._L.clv_destroy(self.h)
             self.h = None
@@ -237,7 +242,7 @@ class HipSampler:
         out = (ctypes.c_int64 * 6)()
         check(self._L.clv_launch_info(self.h, out))
         return dict(persistent=bool(out[0]), persist_blocks_per_cu=int(out[1]), n_cu=int(out[2]),
-                    workgroups=int(out[3]), pc_chunks=int(out[4]), stride_grid=int(out[5]))
+                    workgroups=int(out[3]), pc_chunks=int(out[4]))
 
     # ---- peer exchange (world size > 1 through the persistent kernel, include/clvmcmc.h)
     IPC_HANDLE_BYTES = 64
@@ -380,6 +385,10 @@ class HipGroup:
         h = ctypes.c_void_p()
         check(L.clv_group_create(arr, len(shards), _EXCHANGES[exchange], ctypes.byref(h)))
         self.h, self._L, self.shards = h, L, list(shards)
+        for sh in self.shards:  # back-references: a shard's close() closes this group first
+            if not hasattr(sh, "_groups"):
+                sh._groups = weakref.WeakSet()
+            sh._groups.add(self)
 
     def run(self, n_sweeps: int) -> None:
         check(self._L.clv_group_run(self.h, int(n_sweeps)))
@@ -392,6 +401,10 @@ class HipGroup:
         if getattr(self, "h", None):
             self._L.clv_group_destroy(self.h)
             self.h = None
+        for sh in getattr(self, "shards", ()):
+            g = getattr(sh, "_groups", None)
+            if g is not None:
+                g.discard(self)
 
     def __del__(self):
         try:

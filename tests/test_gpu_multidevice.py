@@ -90,6 +90,7 @@ def test_group_p2p_timeout_falls_back_to_copy(monkeypatch):
         shards.append(HipSampler(Dm.slice_problem(p, b, e), n_global=p.N, shard_begin=r * plan.blocks_per_rank * 256,
                                  world_size=2, rank=r, blocks_per_rank=plan.blocks_per_rank,
                                  blocks_per_unit=plan.blocks_per_unit, prior=prior, device=0, **kw))
+    g = None
     try:
         g = HipGroup(shards, "p2p")
         assert g.exchange == "p2p" and all(sh.p2p_info()["connected"] for sh in shards)
@@ -108,6 +109,8 @@ def test_group_p2p_timeout_falls_back_to_copy(monkeypatch):
             assert np.array_equal(bits(sums), bits(ref_sums[:, :, b:e]))
             assert sh.p2p_info()["mail_memory"] in ("uncached", "fine-grained", "device")
     finally:
+        if g is not None:  # the group before its shards (clv_group_destroy touches the shards)
+            g.close()
         for sh in shards:
             sh.close()
 

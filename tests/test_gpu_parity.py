@@ -475,11 +475,11 @@ def test_device_fast_log_accuracy(L):
     assert np.mean(out == ref) > 0.6
 
 
-def _run_mode(p, persistent, sweeps, chunks, stride=False, **kw):
+def _run_mode(p, persistent, sweeps, chunks, **kw):
     """Run `sweeps` sweeps in clv_run calls of `chunks` sizes with the persistent kernel on/off
-    (off: the stride kernel if `stride`, else one launch per sweep)."""
+    (off: one launch per sweep)."""
     from mcmc_clv_model_amd.sampler import HipSampler
-    env = {"CLV_PERSISTENT": "1" if persistent else "0", "CLV_STRIDE": "1" if stride else "0"}
+    env = {"CLV_PERSISTENT": "1" if persistent else "0"}
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:
@@ -532,37 +532,6 @@ def test_persistent_kernel_bitwise_equals_launch_per_sweep(L, monkeypatch, D, co
     assert a[0]["persistent"] and not b[0]["persistent"], (a[0], b[0])
     if D == 2 and n == 23570:  # 3 chains x 94 workgroups on 256 CUs: MH-variate producers / consumers
         assert a[0]["pc_chunks"] == 3, a[0]
-    for x, y in zip(a[1], b[1]):
-        assert np.array_equal(bits(x), bits(y))
-    for x, y in zip(a[2:], b[2:]):
-        if x is not None:
-            assert np.array_equal(bits(x), bits(y))
-
-
-@pytest.mark.parametrize("D,covs,n,chains,sink,S", [(2, ["first_sales_scaled"], 23570, 3, "full", 20),
-                                                    (2, [f"c{k}" for k in range(1, 5)], 150_000, 1, "summary", 20),
-                                                    (2, [], 2357, 2, "summary+pct", 7),
-                                                    (3, ["gender_F", "age_scaled"], 23570, 2, "summary", 20)])
-def test_stride_kernel_bitwise_equals_launch_per_sweep(L, D, covs, n, chains, sink, S):
-    """World size 1, grids too large to be resident (c4 / c5): the stride kernel (one launch for all
-    of a clv_run's sweeps; a resident grid taking (sweep, chain, block) tasks in order, state in
-    HBM, the chain's last unit drawing level 2 while the other workgroups prepare their next
-    tasks) reproduces the launch-per-sweep kernel bit for bit — state, draws, level-2 records,
-    log-likelihood, summaries, percentile store — over uneven clv_run calls, burn-in and thinning,
-    with units of several blocks (150,000 customers: blocks_per_unit 2), a partial last MH chunk
-    (S = 7) and the trivariate instance (forced: CLV_STRIDE=1)."""
-    from mcmc_clv_model_amd.data import synthetic_cbs
-    from mcmc_clv_model_amd.sampler import build_problem
-    if n == 150_000:
-        df = synthetic_cbs(n, 5, 2, seed=77)
-    else:
-        df = cdnow("full", n) if n > 2357 else cdnow("abe", n)
-    p = build_problem(df, covs, D)
-    kw = dict(mcmc=25, burnin=6, thin=3, chains=chains, seed=2026, draw_sink=sink, n_mh_steps=S)
-    chunks = (1, 7, 2, 20, 1)
-    a = _run_mode(p, False, 31, chunks, stride=True, **kw)
-    b = _run_mode(p, False, 31, chunks, stride=False, **kw)
-    assert a[0]["stride_grid"] > 0 and b[0]["stride_grid"] == 0 and not a[0]["persistent"], (a[0], b[0])
     for x, y in zip(a[1], b[1]):
         assert np.array_equal(bits(x), bits(y))
     for x, y in zip(a[2:], b[2:]):

@@ -478,3 +478,80 @@ def test_fast_cos_table_and_method():
         lo, hi = int(lo), int(hi)
         u = ((hi << 32 | lo) >> 11) * 2.0 ** -53
         assert abs(cos2pi(lo, hi) - math.cos(two_pi * u)) <= 1.5e-15
+
+
+def test_sharded_graph_sizes_cover_any_step():
+    """Verdict r3 #4: the RCCL path's torch.cuda graphs.  A step of n sweeps replays chunk-sized
+    graphs and then the binary decomposition of the rest, so the driver's 20-sweep step (chunk 32)
+    replays the 16- and 4-sweep graphs instead of ~5 eager host calls per sweep; every size used is
+    one captured at the first step."""
+    from mcmc_clv_model_amd.distributed import graph_sizes, graph_sizes_all
+    assert graph_sizes(20, 32) == [16, 4]
+    assert graph_sizes(5, 32) == [4, 1]
+    assert graph_sizes(70, 32) == [32, 32, 4, 2]
+    assert graph_sizes(0, 32) == [] and graph_sizes(7, 0) == []
+    assert graph_sizes_all(32) == [32, 16, 8, 4, 2, 1] and graph_sizes_all(24) == [24, 16, 8, 4, 2, 1]
+    for chunk in (1, 3, 24, 32, 64):
+        for n in range(0, 200):
+            g = graph_sizes(n, chunk)
+            assert sum(g) == n and set(g) <= set(graph_sizes_all(chunk))
+
+
+def test_sharded_step_replays_graphs_for_20_sweeps():
+    """ShardedSampler.step on the RCCL path with graph_chunk 32 (bench.py's default) and the
+    driver's 20 steps: graphs are captured once (at the first graph-using step, e.g. the warm-up)
+    and the 20-sweep step replays graphs only — no eager sweeps."""
+    from mcmc_clv_model_amd import distributed as Dm
+
+    class FakeGraph:
+        def __init__(self, k):
+            self.k, self.n = k, 0
+
+        def replay(self):
+            self.n += 1
+
+    class FakeS:
+        done = 0
+
+        def note_sweeps(self, k):
+            self.done += k
+
+    class Stub:
+        torch = __import__("torch")
+        exchange, graph_chunk, timing, graph = "rccl", 32, False, None
+        stream = None
+        s = FakeS()
+        eager = []
+
+        def _capture(self, k):
+            return FakeGraph(k)
+
+        def _eager(self, n):
+            self.eager.append(n)
+
+    import contextlib
+    st = Stub()
+    orig = Stub.torch.cuda.stream
+    Stub.torch.cuda.stream = lambda s: contextlib.nullcontext()
+    try:
+        Dm.ShardedSampler.step(st, 5)      # warm-up: captures every size
+        assert sorted(st.graph) == [1, 2, 4, 8, 16, 32]
+        caps = dict(st.graph)
+        Dm.ShardedSampler.step(st, 20)     # the timed step
+    finally:
+        Stub.torch.cuda.stream = orig
+    assert st.graph == caps and st.eager == [0, 0]
+    assert st.graph[16].n == 1 and st.graph[4].n == 2 and st.graph[1].n == 1 and st.s.done == 25
+
+
+@pytest.mark.parametrize("val,want", [(None, 10000.0), ("300", 300.0), ("0.5", 1.0), ("abc", 1.0), ("", 1.0),
+                                      ("  250ms", 250.0), ("1e3", 1000.0), ("-5", 1.0)])
+def test_run_wait_ms_parses_like_clv_create(monkeypatch, val, want):
+    """the wait bound restored after the peer-path check is parsed as clv_create parses
+    CLV_WAIT_TIMEOUT_MS (atof prefix, clamped to >= 1 ms), so no accepted value raises there."""
+    from mcmc_clv_model_amd.distributed import run_wait_ms
+    if val is None:
+        monkeypatch.delenv("CLV_WAIT_TIMEOUT_MS", raising=False)
+    else:
+        monkeypatch.setenv("CLV_WAIT_TIMEOUT_MS", val)
+    assert run_wait_ms() == want

@@ -1,0 +1,51 @@
+"""Where the driver's 20-sweep c2 step goes (bench.py --steps 20 --warmup 5): host time until
+clv_run returns, then torch.cuda.synchronize(), next to the launch's event-timed duration; and the
+same launch right after a long one (GPU clocks ramped) to separate the clock ramp from fixed costs.
+One JSON line per case into stdout."""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from bench import load_workload  # noqa: E402
+from mcmc_clv_model_amd.sampler import HipSampler, build_problem  # noqa: E402
+
+
+def main():
+    reps = int(os.environ.get("REPS", "5"))
+    n = int(os.environ.get("NSWEEPS", "20"))
+    df, D, covs, chains, burnin, mcmc, thin, sink = load_workload("c2")
+    p = build_problem(df, covs, D)
+    s = HipSampler(p, mcmc=mcmc, burnin=burnin, thin=thin, chains=chains, seed=42, draw_sink=sink, device=0)
+    s.run(5)
+    s.synchronize()
+    for case in ("cold", "after_long"):
+        for r in range(reps):
+            if case == "after_long":
+                s.run(2000)
+            else:
+                time.sleep(0.2)  # the driver's command: seconds of host work before the timed step
+                s.run(5)
+            s.synchronize()
+            torch.cuda.synchronize()
+            s.set_timing(True)
+            t0 = time.perf_counter()
+            s.run(n)
+            t1 = time.perf_counter()
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+            kt = s.kernel_time()
+            s.set_timing(False)
+            print(json.dumps(dict(case=case, rep=r, sweeps=n, run_us=round((t1 - t0) * 1e6, 2),
+                                  sync_us=round((t2 - t1) * 1e6, 2), wall_us=round((t2 - t0) * 1e6, 2),
+                                  kernel_us=round(kt["sweep_ms"] * 1e3, 2),
+                                  us_per_step=round((t2 - t0) * 1e6 / n, 3))), flush=True)
+    s.close()
+
+
+if __name__ == "__main__":
+    main()
