@@ -225,6 +225,11 @@ int clv_debug_philox(uint32_t k0, uint32_t k1, const uint32_t* ctr, int64_t n, u
 int clv_debug_variates(uint64_t seed, int32_t chain, uint32_t sweep, int64_t n, int32_t n_steps,
                        float* t_l, float* t_m, float* u_acc, double* u_z, double* u_tau,
                        double* e_alive, double* eta_z);
+/* The MH proposal's Student-t(3) transforms on caller words (n x 3 uint32: radius word of t_l,
+ * radius word of t_m, angle word: t_l takes its high 16 bits, t_m its low 16 bits), as the sweep
+ * kernels form them (packed 0: t3_f32, 1: the trivariate launch-per-sweep kernels' t3_pair).
+ * Pins the proposal's symmetry (bi:316-317 draws Sigma[0,0] * standard_t(3)). */
+int clv_debug_t3(const uint32_t* words, int64_t n, int32_t packed, float* t_l, float* t_m);
 /* Level-2 draw from given sufficient statistics and variates (replaces bi:233-262 given rng):
  * xty K*D, yty D*D, iw_normal n_tril, iw_chi2 D, z D*K (standard normals) -> beta, Sigma. */
 int clv_debug_level2(int32_t D, int32_t K, const clv_prior* prior, const double* xty,

@@ -1290,6 +1290,21 @@ int clv_debug_variates(uint64_t seed, int32_t chain, uint32_t sweep, int64_t n, 
   return CLV_OK;
 }
 
+int clv_debug_t3(const uint32_t* words, int64_t n, int32_t packed, float* tl, float* tm) {
+  if (!words || !tl || !tm || n < 1 || (packed != 0 && packed != 1)) return fail(CLV_EINVAL, "bad arguments");
+  uint32_t* dw = nullptr;
+  float *dl = nullptr, *dm = nullptr;
+  CLV_HIP(dalloc(&dw, 3 * n));
+  CLV_HIP(dalloc(&dl, n));
+  CLV_HIP(dalloc(&dm, n));
+  CLV_HIP(hipMemcpy(dw, words, 12 * n, hipMemcpyHostToDevice));
+  CLV_HIP(launch_debug_t3(dw, n, packed, dl, dm, nullptr));
+  CLV_HIP(hipMemcpy(tl, dl, sizeof(float) * n, hipMemcpyDeviceToHost));
+  CLV_HIP(hipMemcpy(tm, dm, sizeof(float) * n, hipMemcpyDeviceToHost));
+  for (void* p : {(void*)dw, (void*)dl, (void*)dm}) CLV_HIP(hipFree(p));
+  return CLV_OK;
+}
+
 int clv_debug_level2(int32_t D, int32_t K, const clv_prior* prior, const double* xty, const double* yty,
                      const double* iwn, const double* chi2, const double* z, double* beta, double* sigma) {
   if ((D != 2 && D != 3) || K < 1 || K > CLV_MAX_K || !prior) return fail(CLV_EINVAL, "bad arguments");

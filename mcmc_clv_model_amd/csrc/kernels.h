@@ -156,6 +156,7 @@ hipError_t launch_debug_philox(uint32_t k0, uint32_t k1, const uint32_t* ctr, in
 hipError_t launch_debug_variates(uint64_t seed, int chain, uint32_t sweep, int64_t n, int S, float* tl,
                                  float* tm, float* ua, double* uz, double* ut, double* ea, double* ez,
                                  hipStream_t st);
+hipError_t launch_debug_t3(const uint32_t* w, int64_t n, int packed, float* tl, float* tm, hipStream_t st);
 hipError_t launch_debug_level2(int D, int K, const double* prior_dev, const double* in, double* out,
                                hipStream_t st);
 hipError_t launch_debug_hyper_variates(uint64_t seed, int chain, uint32_t sweep, double df, int64_t n,

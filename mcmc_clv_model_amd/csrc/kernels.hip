@@ -2417,6 +2417,23 @@ __global__ void debug_variates_kernel(uint64_t seed, int chain, uint32_t sweep, 
   }
 }
 
+// The MH proposal's t3 transforms on caller words (n x 3: radius words x, y and the angle word z),
+// exactly as mh_chunk_variates forms them: packed = 0 -> t3_f32 (the bivariate and persistent
+// kernels), 1 -> t3_pair (trivariate launch-per-sweep).  Pins the proposal's symmetry (tests).
+__global__ void debug_t3_kernel(const uint32_t* w, int64_t n, int packed, float* tl, float* tm) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t x = w[3 * i], y = w[3 * i + 1], z = w[3 * i + 2];
+  if (packed) {
+    const f32x2 t = t3_pair(x, y, z);
+    tl[i] = t.x;
+    tm[i] = t.y;
+  } else {
+    tl[i] = t3_f32(uf32(x), angle_hi(z));
+    tm[i] = t3_f32(uf32(y), angle_lo(z));
+  }
+}
+
 // in: [V 81][cholV 81][A0B0 27][S0B 9] prior block, then xty(K*D) yty(D*D) iwn(3) chi2(3) z(D*K)
 template <int D, int K>
 __global__ void debug_level2_kernel(const double* prior, const double* in, double* out) {
@@ -2601,6 +2618,11 @@ hipError_t launch_debug_variates(uint64_t seed, int chain, uint32_t sweep, int64
                                  hipStream_t st) {
   hipLaunchKernelGGL(debug_variates_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, seed, chain,
                      sweep, n, S, tl, tm, ua, uz, ut, ea, ez);
+  return hipGetLastError();
+}
+
+hipError_t launch_debug_t3(const uint32_t* w, int64_t n, int packed, float* tl, float* tm, hipStream_t st) {
+  hipLaunchKernelGGL(debug_t3_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, w, n, packed, tl, tm);
   return hipGetLastError();
 }
 

@@ -455,6 +455,36 @@ def test_device_fast_exp_accuracy(L):
     assert np.mean(out == ref) > 0.6
 
 
+@pytest.mark.parametrize("packed", [0, 1])
+def test_t3_proposal_symmetric_over_every_angle(L, packed):
+    """Verdict r3: the random-walk proposal of the production MH step is symmetric, so the MH
+    acceptance of bi:316-330 (which omits the proposal ratio) stays exact.  t3 = R cos(2 pi V) with
+    V on the 2^16-point angle lattice (philox.h t3_f32 / t3_pair, hardware v_cos_f32): for fixed
+    radius words, every angle of both 16-bit halves is run through the device transform, and the
+    multiset of the 65,536 values must equal its negation exactly (R >= 0 is independent of V, so
+    this is the proposal's symmetry).  Also pinned: the packed pair equals the scalar form bit for
+    bit, and the stronger pairwise identity t(k + 2^15) == -t(k) for every angle k."""
+    k = np.arange(65536, dtype=np.uint32)
+    radius = [0, 1, 0x7FFFFFFF, 0x80000000, 0xFFFFFFFF, 0x12345678, 0x9E3779B9, 0x00C0FFEE]
+    n = len(k)
+    for rw in radius:
+        w = np.empty((n, 3), np.uint32)
+        w[:, 0] = rw
+        w[:, 1] = rw
+        w[:, 2] = (k << 16) | k
+        outs = {}
+        for pk in (0, packed):
+            tl, tm = np.empty(n, np.float32), np.empty(n, np.float32)
+            assert L.clv_debug_t3(_u32p(np.ascontiguousarray(w)), n, pk, _fp(tl), _fp(tm)) == 0
+            outs[pk] = (tl, tm)
+        tl, tm = outs[packed]
+        assert np.array_equal(bits(tl), bits(outs[0][0])) and np.array_equal(bits(tm), bits(outs[0][1]))
+        assert np.array_equal(tl, tm)  # the same angle in either half gives the same variate
+        assert np.isfinite(tl).all() and (np.abs(tl).max() > 0 or rw == 0xFFFFFFFF)
+        assert np.array_equal(np.sort(tl), np.sort(-tl)), f"radius word {rw:#x}: t3 multiset not symmetric"
+        assert np.array_equal(tl, -np.roll(tl, -32768)), f"radius word {rw:#x}: t(k + 2^15) != -t(k)"
+
+
 def test_device_fast_log_accuracy(L):
     """log_fast (csrc/fastmath.h), the Philox-mode logs of the z/tau draw (bi:200-225: log lambda,
     log mu, the dropout time's uniform / truncated-exponential argument) and eta's normal:
