@@ -206,18 +206,23 @@ def cpu_baseline(workload: str, warm: int = 20, timed: int = 200, parallel: bool
 
 
 def measure_config(name: str, world: int, rank: int, local_rank: int, dist, steps: int, warmup: int,
-                   graph_chunk: int, exchange: str) -> dict:
+                   graph_chunk: int, exchange: str, stored_phase: bool = True) -> dict:
     """One BASELINE multi-GPU configuration at this world size: c4 = 1M bivariate
     customers K=5 sharded over the ranks (strong scaling: the same problem at every N), c5 = 1.25M
     trivariate customers K=9 per rank (weak scaling).  Wall time of `steps` sweeps (max over ranks)
-    after `warmup` sweeps; HBM fraction of the algorithmic bytes against N x 8 TB/s."""
+    after `warmup` sweeps; HBM fraction of the algorithmic bytes against N x 8 TB/s.  With
+    `stored_phase` (and a burn-in longer than the window) the same chains then continue past the
+    burn-in and `steps` stored sweeps are timed too (`stored`: each also read-modify-writes the
+    customer's running sums), and `whole_run` combines both phases' per-sweep times over the
+    BASELINE run's burn-in + mcmc sweeps."""
     import torch
     from mcmc_clv_model_amd.sampler import HipSampler, build_problem
     df, D, covs, chains, burnin, mcmc, thin, sink = load_workload(name, world)
     n_total = len(df)
     p = build_problem(df, covs, D)
     del df
-    mcmc = max(mcmc, warmup + steps - burnin)
+    mcmc0 = mcmc
+    mcmc = max(mcmc, warmup + steps - burnin, 100 + steps)
     if world == 1:
         kern = HipSampler(p, mcmc=mcmc, burnin=burnin, thin=thin, chains=chains, seed=42, draw_sink=sink,
                           device=local_rank)
@@ -229,22 +234,48 @@ def measure_config(name: str, world: int, rank: int, local_rank: int, dist, step
                               verify_sweeps=8)
         run, sync = kern.step, kern.synchronize
     del p
+
+    def timed(n: int) -> float:
+        """Wall time of n sweeps bracketed by barrier + synchronize, max over ranks."""
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        run(n)
+        sync()
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        if dist:
+            t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local_rank}")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        return dt
+
     run(warmup)
     sync()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    run(steps)
-    sync()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local_rank}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    dt = timed(steps)  # burn-in sweeps warmup+1 .. warmup+steps
+    # the stored phase (verdict r3: half of the BASELINE run; every sweep after burn-in
+    # read-modify-writes the customer's running sums, bi:402-428): continue the same chains into
+    # it, 100 sweeps past the boundary (warm), then time `steps` stored sweeps
+    phases = None
+    if stored_phase and burnin > warmup + steps:
+        done = warmup + steps
+        run(burnin + 100 - done)
+        sync()
+        dt_st = timed(steps)
+        first = burnin + 101
+        bpu_st = algorithmic_bytes(D, len(covs) + 1, stored_fraction(burnin, thin, first, first + steps - 1), sink)
+        v_st = chains * n_total * steps / dt_st
+        t_b, t_s = dt / steps, dt_st / steps  # s per sweep in each phase
+        whole = chains * n_total * (burnin + mcmc0) / (burnin * t_b + mcmc0 * t_s)
+        phases = dict(
+            stored=dict(value=v_st, ms_per_step=t_s * 1e3, sweeps=f"{first}..{first + steps - 1}",
+                        bytes_per_unit=round(bpu_st, 2),
+                        hbm_frac=round(bpu_st * v_st / 1e9 / (world * HBM_PEAK_GBS), 5)),
+            whole_run=dict(value=whole, sweeps=f"{burnin} burn-in + {mcmc0} stored",
+                           note="customer-sweeps/s of the BASELINE run from the two phases' per-sweep times"))
     linfo = kern.launch_info()
     persistent = linfo["persistent"]
     exch = getattr(kern, "exchange", None)
@@ -265,7 +296,8 @@ def measure_config(name: str, world: int, rank: int, local_rank: int, dist, step
                      ("" if world == 1 else
                       (", unit partials stored into every rank's mail over xGMI by the kernel (no host collective)"
                        if exch == "p2p" else ", RCCL all-gather + level-2 kernel per sweep") +
-                      (f" ({note})" if note else "")))
+                      (f" ({note})" if note else "")),
+                phase=f"burn-in (sweeps {warmup + 1}..{warmup + steps})", **(phases or {}))
 
 
 def main():
@@ -463,7 +495,7 @@ def main():
         # BASELINE configs[0] ("Bivariate M1, Abe 1/10 CDNOW subset, 4000 iters on CPU numpy reference
         # path"): the same 4-chain c1 sampler on the GPU (2,000 sweeps after 80), next to its 1-core
         # CPU leg in cpu_baseline["c1"]
-        extra["c1"] = measure_config("c1", 1, rank, local_rank, None, 2000, 80, 0, "rccl")
+        extra["c1"] = measure_config("c1", 1, rank, local_rank, None, 2000, 80, 0, "rccl", stored_phase=False)
 
     if rank == 0:
         cpu = None

@@ -555,3 +555,52 @@ def test_run_wait_ms_parses_like_clv_create(monkeypatch, val, want):
     else:
         monkeypatch.setenv("CLV_WAIT_TIMEOUT_MS", val)
     assert run_wait_ms() == want
+
+
+def test_bench_config_times_the_stored_phase(monkeypatch):
+    """Verdict r3 #3: the c4 / c5 lines time a burn-in window AND a window of stored sweeps (the
+    running-sum read-modify-write of bi:402-428, summary sink), continuing the same chains past the
+    burn-in, and combine both into the whole BASELINE run's rate.  Stub sampler, no GPU."""
+    import torch
+
+    import bench
+    from mcmc_clv_model_amd import sampler as S
+
+    log = []
+
+    class Fake:
+        def __init__(self, p, **kw):
+            self.kw, self.done = kw, 0
+
+        def run(self, n):
+            log.append((self.done + 1, self.done + n))
+            self.done += n
+
+        def synchronize(self):
+            pass
+
+        def launch_info(self):
+            return dict(persistent=False)
+
+        def close(self):
+            pass
+
+    monkeypatch.setattr(S, "HipSampler", Fake)
+    monkeypatch.setattr(S, "build_problem", lambda df, covs, D: None)
+    monkeypatch.setattr(torch.cuda, "synchronize", lambda *a, **k: None)
+    monkeypatch.setitem(bench.WORKLOADS, "c4", bench.WORKLOADS["c4"][:1] + ("synthetic:500:5:20250718",)
+                        + bench.WORKLOADS["c4"][2:])
+    r = bench.measure_config("c4", 1, 0, 0, None, 1000, 200, 0, "rccl")
+    burnin = bench.WORKLOADS["c4"][4]
+    assert log == [(1, 200), (201, 1200), (1201, burnin + 100), (burnin + 101, burnin + 1100)]
+    assert r["phase"].startswith("burn-in") and r["stored"]["sweeps"] == f"{burnin + 101}..{burnin + 1100}"
+    D, K = 2, 5
+    assert r["bytes_per_unit"] == round(bench.algorithmic_bytes(D, K, 0.0, "summary"), 2) == 84.0
+    assert r["stored"]["bytes_per_unit"] == 84.0 + 144.0
+    tb, ts = r["ms_per_step"], r["stored"]["ms_per_step"]
+    n = 500
+    want = n * 10000 / (5000 * tb + 5000 * ts) * 1e3
+    assert abs(r["whole_run"]["value"] / want - 1) < 1e-9
+    log.clear()
+    r1 = bench.measure_config("c4", 1, 0, 0, None, 1000, 200, 0, "rccl", stored_phase=False)
+    assert log == [(1, 200), (201, 1200)] and "stored" not in r1
