@@ -1,9 +1,11 @@
 """Where the driver's 20-sweep c2 step goes (bench.py --steps 20 --warmup 5): host time until
 clv_run returns, then torch.cuda.synchronize(), next to the launch's event-timed duration; and the
 same launch right after a long one (GPU clocks ramped) to separate the clock ramp from fixed costs.
-One JSON line per case into stdout."""
+Env: REPS, NSWEEPS, TIMING (1: events around the timed launch, as bench.py; 0: none), LABEL.
+One JSON line per case into stdout, then a median line per case."""
 import json
 import os
+import statistics
 import sys
 import time
 
@@ -18,11 +20,14 @@ from mcmc_clv_model_amd.sampler import HipSampler, build_problem  # noqa: E402
 def main():
     reps = int(os.environ.get("REPS", "5"))
     n = int(os.environ.get("NSWEEPS", "20"))
+    timing = os.environ.get("TIMING", "1") == "1"
+    label = os.environ.get("LABEL", "")
     df, D, covs, chains, burnin, mcmc, thin, sink = load_workload("c2")
     p = build_problem(df, covs, D)
     s = HipSampler(p, mcmc=mcmc, burnin=burnin, thin=thin, chains=chains, seed=42, draw_sink=sink, device=0)
     s.run(5)
     s.synchronize()
+    rows = {}
     for case in ("cold", "after_long"):
         for r in range(reps):
             if case == "after_long":
@@ -32,18 +37,26 @@ def main():
                 s.run(5)
             s.synchronize()
             torch.cuda.synchronize()
-            s.set_timing(True)
+            if timing:
+                s.set_timing(True)
             t0 = time.perf_counter()
             s.run(n)
             t1 = time.perf_counter()
             torch.cuda.synchronize()
             t2 = time.perf_counter()
-            kt = s.kernel_time()
-            s.set_timing(False)
-            print(json.dumps(dict(case=case, rep=r, sweeps=n, run_us=round((t1 - t0) * 1e6, 2),
-                                  sync_us=round((t2 - t1) * 1e6, 2), wall_us=round((t2 - t0) * 1e6, 2),
-                                  kernel_us=round(kt["sweep_ms"] * 1e3, 2),
-                                  us_per_step=round((t2 - t0) * 1e6 / n, 3))), flush=True)
+            kt = s.kernel_time() if timing else {"sweep_ms": float("nan")}
+            if timing:
+                s.set_timing(False)
+            row = dict(label=label, case=case, rep=r, sweeps=n, run_us=round((t1 - t0) * 1e6, 2),
+                       sync_us=round((t2 - t1) * 1e6, 2), wall_us=round((t2 - t0) * 1e6, 2),
+                       kernel_us=round(kt["sweep_ms"] * 1e3, 2), us_per_step=round((t2 - t0) * 1e6 / n, 3))
+            rows.setdefault(case, []).append(row)
+            print(json.dumps(row), flush=True)
+    for case, rs in rows.items():
+        med = {k: round(statistics.median(x[k] for x in rs), 2) for k in ("run_us", "sync_us", "wall_us", "kernel_us",
+                                                                        "us_per_step")}
+        print(json.dumps(dict(label=label, case=case, median=med,
+                              env={k: v for k, v in os.environ.items() if k.startswith("CLV_")})), flush=True)
     s.close()
 
 

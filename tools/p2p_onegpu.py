@@ -18,13 +18,25 @@ WORKLOAD = os.environ.get("CLV_P2P_WORKLOAD", "c2")
 WARM = 200 if WORKLOAD in ("c1", "c2", "c3") else 20
 
 
+def load_workload():
+    """bench.load_workload(WORKLOAD); CLV_P2P_N overrides a synthetic workload's customer count
+    (e.g. c4 at 125,000: one 8-rank shard of c4 split over the W processes on this card)."""
+    import bench
+    n = os.environ.get("CLV_P2P_N")
+    if n:
+        D, data, *rest = bench.WORKLOADS[WORKLOAD]
+        _, _, K, seed = data.split(":")
+        bench.WORKLOADS[WORKLOAD] = (D, f"synthetic:{int(n)}:{K}:{seed}", *rest)
+    return bench.load_workload(WORKLOAD)
+
+
 def worker(sweeps):
     import torch.distributed as dist
     import bench
     from mcmc_clv_model_amd.sampler import build_problem
     from mcmc_clv_model_amd.distributed import ShardedSampler
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
-    df, D, covs, ch, burnin, mcmc, thin, sink = bench.load_workload(WORKLOAD)
+    df, D, covs, ch, burnin, mcmc, thin, sink = load_workload()
     p = build_problem(df, covs, D)
     dist.init_process_group("gloo")
     ss = ShardedSampler(p, rank=rank, world=world, chains=ch, mcmc=mcmc, burnin=burnin, thin=thin, seed=42,
@@ -38,8 +50,9 @@ def worker(sweeps):
     dist.barrier()
     dt = time.perf_counter() - t0
     if rank == 0:
-        print(json.dumps(dict(workload=WORKLOAD, world=world, us_per_sweep=dt / sweeps * 1e6, exchange=ss.exchange,
-                              persistent=ss.launch_info()["persistent"], note=ss.p2p_note)))
+        print(json.dumps(dict(workload=WORKLOAD, n=len(df), world=world, us_per_sweep=dt / sweeps * 1e6,
+                              exchange=ss.exchange, persistent=ss.launch_info()["persistent"], note=ss.p2p_note,
+                              env={k: v for k, v in os.environ.items() if k.startswith("CLV_")})), flush=True)
     if os.environ.get("CLV_LIB_PATH", "").endswith("_stamps.so"):  # level-2 workgroup timeline, one sweep
         import ctypes
         import numpy as np
@@ -71,7 +84,7 @@ def main(world=2, sweeps=3000):
                                        MASTER_PORT=str(port))) for r in range(world)]
     rc = [p.wait(timeout=300) for p in procs]
     assert rc == [0] * world, rc
-    df, D, covs, ch, burnin, mcmc, thin, sink = bench.load_workload(WORKLOAD)
+    df, D, covs, ch, burnin, mcmc, thin, sink = load_workload()
     with HipSampler(build_problem(df, covs, D), mcmc=mcmc, burnin=burnin, thin=thin, chains=ch, seed=42,
                     draw_sink=sink) as s:
         s.run(WARM)
