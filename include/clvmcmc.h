@@ -219,6 +219,10 @@ int clv_kernel_time(clv_sampler* s, double* sweep_kernel_ms_total, int64_t* swee
                     double* hyper_kernel_ms_total, int64_t* hyper_launches);
 
 /* ---- test hooks (run the device code paths on caller data) ---- */
+/* Host clock (steady_clock ns) at the steps of the last persistent clv_run at world size 1:
+ * out[0] entry, [1] after hipSetDevice, [2] before the launch call, [3] after it, [4] launch
+ * enqueued (end event recorded), [5] end seen, [6] return; 0 where not reached. */
+int clv_debug_host_times(const clv_sampler* s, int64_t* out);
 /* Philox4x32-10 on device: ctr/out are n x 4 words. */
 int clv_debug_philox(uint32_t k0, uint32_t k1, const uint32_t* ctr, int64_t n, uint32_t* out);
 /* The Philox-mode variates of one sweep for customers [0, n): t_l/t_m/u_acc are S x n. */

@@ -112,6 +112,7 @@ def lib() -> ctypes.CDLL:
         "clv_debug_philox": (c_int32, [c_uint32, c_uint32, POINTER(c_uint32), c_int64, POINTER(c_uint32)]),
         "clv_debug_variates": (c_int32, [c_uint64, c_int32, c_uint32, c_int64, c_int32, POINTER(c_float),
                                          POINTER(c_float), POINTER(c_float), dp, dp, dp, dp]),
+        "clv_debug_host_times": (c_int32, [sp, POINTER(c_int64)]),
         "clv_debug_t3": (c_int32, [POINTER(c_uint32), c_int64, c_int32, POINTER(c_float), POINTER(c_float)]),
         "clv_debug_level2": (c_int32, [c_int32, c_int32, POINTER(ClvPrior), dp, dp, dp, dp, dp, dp, dp]),
         "clv_debug_hyper_variates": (c_int32, [c_uint64, c_int32, c_uint32, c_double, c_int64, dp, dp]),

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
@@ -888,6 +889,11 @@ int clv_note_sweeps(clv_sampler* s, int64_t n) {
 // Persistent path: one launch of persist_kernel for all n sweeps (see kernels.hip), in two halves
 // so that a group of shards in one process (group.hip) can have every shard's launch in flight
 // before waiting for any.
+static inline int64_t host_now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
 int clv::persist_launch(clv_sampler* s, int64_t n_sweeps) {
   const Geometry& g = s->g;
   s->last_persist_n = 0;
@@ -917,10 +923,14 @@ int clv::persist_launch(clv_sampler* s, int64_t n_sweeps) {
                                  // less host cost on the driver's 20-sweep run than the dispatch's
                                  // own timestamps (hipExtLaunchKernelGGL), same duration to 0.2%
     CLV_HIP(hipEventRecord(e0, s->stream));
+    s->host_ns[2] = host_now_ns();
     CLV_HIP(launch_persist(a, s->sweeps_done + 1, n_sweeps, s->stream, nullptr, nullptr));
+    s->host_ns[3] = host_now_ns();
     CLV_HIP(hipEventRecord(e1, s->stream));
   } else {
+    s->host_ns[2] = host_now_ns();
     CLV_HIP(launch_persist(a, s->sweeps_done + 1, n_sweeps, s->stream, e0, e1));
+    s->host_ns[3] = host_now_ns();
   }
   // the launch's end event (timing: the dispatch's own end timestamp; else one recorded behind
   // it).  Timed launches are harvested later (clv_kernel_time or a full slot set).
@@ -936,6 +946,7 @@ int clv::persist_launch(clv_sampler* s, int64_t n_sweeps) {
     s->inflight_done = s->done_ev;
   }
   s->inflight_n = n_sweeps;
+  s->host_ns[4] = host_now_ns();
   return CLV_OK;
 }
 
@@ -955,6 +966,7 @@ int clv::persist_wait(clv_sampler* s) {
   } else {
     CLV_HIP(hipEventSynchronize(done));
   }
+  s->host_ns[5] = host_now_ns();
   if (__atomic_load_n(s->h_abort, __ATOMIC_ACQUIRE)) {
     // the carried state was written to the *_alt buffers only: lam / mu / hyper still hold the
     // state this launch started from; restore the counters, flags and running sums
@@ -1085,7 +1097,9 @@ int clv_run(clv_sampler* s, int64_t n_sweeps) {
     return run_fused_exchange(s, n_sweeps);
   }
   if (n_sweeps < 0) return fail(CLV_EINVAL, "n_sweeps < 0");
+  s->host_ns[0] = host_now_ns();
   CLV_HIP(hipSetDevice(s->device));
+  s->host_ns[1] = host_now_ns();
   int rc = check_replay_range(s, n_sweeps);
   if (rc) return rc;
   if (s->pending_init_hyper) {
@@ -1093,7 +1107,11 @@ int clv_run(clv_sampler* s, int64_t n_sweeps) {
     if (rc) return rc;
     s->pending_init_hyper = false;
   }
-  if (s->persistent) return run_persistent(s, n_sweeps);
+  if (s->persistent) {
+    rc = run_persistent(s, n_sweeps);
+    s->host_ns[6] = host_now_ns();
+    return rc;
+  }
   rc = enqueue_fused_sweeps(s, n_sweeps);
   if (rc) return rc;
   CLV_HIP(hipStreamSynchronize(s->stream));
@@ -1246,6 +1264,12 @@ int clv_debug_wg_stamps(clv_sampler* s, uint64_t* out) {
   CLV_HIP(hipStreamSynchronize(s->stream));
   CLV_HIP(hipMemcpy(out, s->d_stamps + 1024 * 8, sizeof(uint64_t) * 12 * s->g.n_chains * (s->g.nb_local + 1),
                     hipMemcpyDeviceToHost));
+  return CLV_OK;
+}
+
+int clv_debug_host_times(const clv_sampler* s, int64_t* out) {
+  if (!s || !out) return fail(CLV_EINVAL, "bad arguments");
+  for (int k = 0; k < 8; ++k) out[k] = s->host_ns[k];
   return CLV_OK;
 }
 

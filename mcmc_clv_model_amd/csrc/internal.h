@@ -133,6 +133,10 @@ struct clv_sampler {
   bool timing_record = true;        // timed persistent launches bracketed by hipEventRecord
                                     // (CLV_TIMING_RECORD=0: the dispatch's own timestamps)
 
+  // host clock (steady_clock, ns) at the steps of the last persistent clv_run: entry, after
+  // hipSetDevice, before the launch call, after it, after the end-event record, wait done, return
+  int64_t host_ns[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+
   bool timing = false;
   std::vector<hipEvent_t> ev;  // 4 per slot: sweep start/end, hyper start/end
   std::vector<int64_t> ev_sweeps;  // sweeps per timed launch (persistent launches time many)

@@ -3,6 +3,7 @@ clv_run returns, then torch.cuda.synchronize(), next to the launch's event-timed
 same launch right after a long one (GPU clocks ramped) to separate the clock ramp from fixed costs.
 Env: REPS, NSWEEPS, TIMING (1: events around the timed launch, as bench.py; 0: none), LABEL.
 One JSON line per case into stdout, then a median line per case."""
+import ctypes
 import json
 import os
 import statistics
@@ -44,17 +45,25 @@ def main():
             t1 = time.perf_counter()
             torch.cuda.synchronize()
             t2 = time.perf_counter()
+            hn = (ctypes.c_int64 * 8)()
+            assert s._L.clv_debug_host_times(s.h, hn) == 0
+            h = [x / 1e3 for x in hn]  # us
+            host = dict(setdev=round(h[1] - h[0], 2), pre_launch=round(h[2] - h[1], 2), launch=round(h[3] - h[2], 2),
+                        post_launch=round(h[4] - h[3], 2), wait=round(h[5] - h[4], 2), epilogue=round(h[6] - h[5], 2),
+                        outside=round((t1 - t0) * 1e6 - (h[6] - h[0]), 2))
             kt = s.kernel_time() if timing else {"sweep_ms": float("nan")}
             if timing:
                 s.set_timing(False)
             row = dict(label=label, case=case, rep=r, sweeps=n, run_us=round((t1 - t0) * 1e6, 2),
                        sync_us=round((t2 - t1) * 1e6, 2), wall_us=round((t2 - t0) * 1e6, 2),
-                       kernel_us=round(kt["sweep_ms"] * 1e3, 2), us_per_step=round((t2 - t0) * 1e6 / n, 3))
+                       kernel_us=round(kt["sweep_ms"] * 1e3, 2), us_per_step=round((t2 - t0) * 1e6 / n, 3),
+                       host=host)
             rows.setdefault(case, []).append(row)
             print(json.dumps(row), flush=True)
     for case, rs in rows.items():
         med = {k: round(statistics.median(x[k] for x in rs), 2) for k in ("run_us", "sync_us", "wall_us", "kernel_us",
                                                                         "us_per_step")}
+        med["host"] = {k: round(statistics.median(x["host"][k] for x in rs), 2) for k in rs[0]["host"]}
         print(json.dumps(dict(label=label, case=case, median=med,
                               env={k: v for k, v in os.environ.items() if k.startswith("CLV_")})), flush=True)
     s.close()
