@@ -2254,6 +2254,7 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
   }
 
   // ================= customer workgroups =================
+  CLV_P_STAMP(a.stamps, wgi, 7, tid == 0);  // (diagnostic build) this workgroup's first instruction
   Cust<D, K> cu;
   {
     const int64_t i = (int64_t)b * BLOCK + tid;
@@ -2272,6 +2273,7 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
   if constexpr (D == 3) {
     if (cu.active && pre) zeta_lds[tid] = eta_normal(k0, k1, cu.gi, s_first, exp_tab);
   }
+  CLV_P_STAMP(a.stamps, wgi, 10, tid == 0);  // (diagnostic build) prologue done
   const SweepArgs& a_launch = a;
   for (int64_t it = 0; it < n_sweeps; ++it) {
     // bivariate: the arguments re-read through an opaque kernarg pointer each sweep (scalar loads
