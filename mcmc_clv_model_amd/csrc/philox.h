@@ -138,7 +138,10 @@ __device__ __forceinline__ float log2_f32(float u) {  // v_log_f32 (the MH step 
 // 62:779-781): R^2 = nu (U^(-2/nu) - 1) is the squared radius of a spherical bivariate t_nu, so
 // R cos(2 pi V) is exactly t_nu.  Four hardware transcendentals, no rejection.  The radius
 // uniform u is a full 32-bit word; the angle v (revolutions, v_cos_f32) has 16-bit resolution —
-// a symmetric lattice of angles, so the proposal stays symmetric and MH stays exact.
+// a lattice closed under v -> v + 1/2, and the hardware cosine is odd under that shift bit for bit
+// (t(k + 2^15) == -t(k) for all 65,536 angles k, tests/test_gpu_parity.py
+// test_t3_proposal_symmetric_over_every_angle), so the proposal is exactly symmetric and the MH
+// acceptance without a proposal ratio (bi:329-330) targets the reference's posterior.
 __device__ __forceinline__ float t3_f32(float u, float v) {
   const float p = __builtin_amdgcn_exp2f(-(2.0f / 3.0f) * __builtin_amdgcn_logf(u));  // U^(-2/3)
   const float r = __builtin_amdgcn_sqrtf(__builtin_fmaf(3.0f, p, -3.0f));  // 3 (p - 1), one rounding

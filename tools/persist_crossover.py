@@ -14,6 +14,10 @@ sys.path.insert(0, ROOT)
 CASES = [(2, 2, 4, 20000), (2, 2, 4, 26000), (2, 2, 4, 30000),
          (2, 5, 1, 60000), (2, 5, 1, 90000), (2, 5, 1, 110000), (2, 5, 1, 125000),
          (3, 3, 4, 20000), (3, 3, 4, 26000)]
+if os.environ.get("CROSSOVER_SET") == "2":  # chains vs covariates vs model, separated
+    CASES = [(2, 5, 4, 20000), (2, 5, 4, 26000), (2, 2, 1, 60000), (2, 2, 1, 90000), (2, 2, 1, 110000),
+             (2, 9, 1, 60000), (2, 9, 1, 90000), (3, 9, 1, 60000), (3, 3, 1, 90000), (3, 3, 1, 110000),
+             (2, 2, 2, 60000), (2, 2, 4, 28000)]
 
 
 def main():
