@@ -323,6 +323,9 @@ def main():
     ap.add_argument("--scaling-steps", type=int, default=1000)
     ap.add_argument("--blocks-per-unit", type=int, default=0,
                     help="(world size 1, A/B) blocks per statistics unit instead of the plan's (0)")
+    ap.add_argument("--phase", default="burnin", choices=["burnin", "stored"],
+                    help="(profiling) stored: the sampler's burn-in is 0, so every timed sweep is a stored sweep "
+                         "(the running sums' read-modify-write / the draws' stores of bi:402-428)")
     ap.add_argument("--no-c1-leg", dest="c1_leg", action="store_false",
                     help="skip BASELINE configs[0] (c1 on the GPU and its 1-core CPU leg)")
     ap.add_argument("--one-gpu-rehearsal", action="store_true",
@@ -365,6 +368,8 @@ def main():
     from mcmc_clv_model_amd.sampler import HipSampler, build_problem
 
     df, D, covs, chains, burnin, mcmc, thin, sink = load_workload(a.workload, world)
+    if a.phase == "stored":
+        mcmc, burnin = mcmc + burnin, 0
     total = a.warmup + a.steps + (0 if a.no_kernel_timing else min(a.steps, a.timing_steps))
     mcmc_workload = mcmc
     mcmc = max(mcmc, total - burnin)  # draw buffers also cover the sweeps of the roofline pass
@@ -521,6 +526,7 @@ def main():
             config=dict(workload=f"{a.workload}: {'bivariate' if D == 2 else 'trivariate'} M2, covariates {covs}",
                         n_customers=n_total, chains=chains, n_mh_steps=20, burnin=burnin, mcmc=mcmc_workload,
                         thin=thin, seed=42, draw_sink=sink, parallelism=f"customer-shard x{world}",
+                        **({"phase": "stored (profiling: burn-in 0, every sweep stores)"} if a.phase == "stored" else {}),
                         timed_region=(f"one persistent-kernel launch of {a.steps} sweeps" if persistent else
                                       "hipGraph replay of fused sweep launches") if not sharded else
                         (f"one persistent-kernel launch of {a.steps} sweeps per rank, unit partials stored into "

@@ -2160,6 +2160,9 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
   return;
 }
 
+#ifndef CLV_PC_BUILD  // (A/B: 0 compiles the producer / consumer hand-off out of the persistent kernel)
+#define CLV_PC_BUILD 1
+#endif
 // ---- MH-variate producers and consumers (persistent kernel, world size 1; capi.hip pc_plan) ----
 // c2 runs 1,473 customer wavefronts on 1,024 SIMDs: the SIMDs of the CUs that hold two workgroups
 // run two wavefronts and set the sweep period, the others idle part of it.  The drawn-ahead MH
@@ -2276,7 +2279,7 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
   // producer / consumer role of this (dispatch-order) workgroup; none in the P2P instance
   const int T_wg = gridDim.x * gridDim.y, L_wg = blockIdx.y * gridDim.x + blockIdx.x;
   int pc_off = 0, pc_ntask = 0;
-  if (!P2P && a.pc_desc) {
+  if (!P2P && CLV_PC_BUILD && a.pc_desc) {
     pc_off = a.pc_desc[L_wg * PC_DESC];
     pc_ntask = a.pc_desc[L_wg * PC_DESC + 1];
   }

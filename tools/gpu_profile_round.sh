@@ -14,7 +14,9 @@ for W in "$@"; do
     c2|c3|c1) TR="--steps 19000 --warmup 1000"; PS=20000 ;;  # PMC: the whole 20,000-sweep workload, one dispatch
     *)        TR="--steps 2000 --warmup 200 --timing-steps 500"; PS=100 ;;
   esac
-  B="python3 $R/bench.py --workload $W --no-cpu-baseline --scaling-configs="
+  # "<w>stored": workload <w> with every sweep a stored sweep (bench.py --phase stored)
+  WL=${W%stored}; PH=burnin; [ "$WL" != "$W" ] && PH=stored
+  B="python3 $R/bench.py --workload $WL --phase $PH --no-cpu-baseline --scaling-configs= --no-c1-leg"
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $D/trace -o run --output-format csv -- $B $TR > $D/prof_trace.log 2>&1; rc=$?
   echo ${W}_trace_rc=$rc; tail -1 $D/prof_trace.log | cut -c1-200
   [ $rc -eq 0 ] || exit $rc
