@@ -525,6 +525,11 @@ int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* pri
   }
   if (s->persistent || s->p2p_capable || s->fx_capable) {  // (fused exchange: the snapshot buffers)
     CLV_HIPC(dalloc(&s->d_pblock, (size_t)C * std::max(nb_local, 1) * g.stride));
+    if (s->persistent) {  // deferred level-2 draws (CLV_DEFER=0: every launch draws its last one)
+      const char* env = std::getenv("CLV_DEFER");
+      s->defer = !(env && std::string(env) == "0");
+      if (s->defer) CLV_HIPC(dalloc(&s->d_pend, (size_t)2 * C * g.stride));
+    }
     CLV_HIPC(dalloc(&s->d_lam_alt, C * std::max<int64_t>(n, 1)));
     CLV_HIPC(dalloc(&s->d_mu_alt, C * std::max<int64_t>(n, 1)));
     CLV_HIPC(dalloc(&s->d_hyper_alt, C * HS));
@@ -683,7 +688,7 @@ void clv_destroy(clv_sampler* s) {
   if (s->d_unit && s->d_unit != s->d_block) (void)hipFree(s->d_unit);
   if (s->d_hyp2) (void)hipFree(s->d_hyp2);
   for (void* p : {(void*)s->d_lam_alt, (void*)s->d_mu_alt, (void*)s->d_hyper_alt, (void*)s->d_sums_prev,
-                  (void*)s->d_pblock, (void*)s->d_qstore})
+                  (void*)s->d_pblock, (void*)s->d_qstore, (void*)s->d_pend})
     if (p) (void)hipFree(p);
   if (s->h_abort) (void)hipHostFree(s->h_abort);
   for (void* p : s->ipc_opened) (void)hipIpcCloseMemHandle(p);
@@ -717,6 +722,10 @@ int clv_hyper(clv_sampler* s, const double* gathered) {
   if (!s) return fail(CLV_EINVAL, "null sampler");
   if (s->g.world_size > 1 && !gathered) return fail(CLV_EINVAL, "sharded hyper needs the gathered buffer");
   CLV_HIP(hipSetDevice(s->device));
+  {
+    int rc = persist_flush(s);
+    if (rc) return rc;
+  }
   if (s->pending_init_hyper) {
     int rc = check_replay_range(s, 0);
     if (rc) return rc;
@@ -732,7 +741,9 @@ int clv_sweep(clv_sampler* s) {
   if (!s) return fail(CLV_EINVAL, "null sampler");
   if (s->pending_init_hyper) return fail(CLV_ESTATE, "bivariate: call clv_hyper once before the first sweep");
   CLV_HIP(hipSetDevice(s->device));
-  int rc = check_replay_range(s, 1);
+  int rc = persist_flush(s);
+  if (rc) return rc;
+  rc = check_replay_range(s, 1);
   if (rc) return rc;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (s->timing) {
@@ -910,6 +921,9 @@ int clv::persist_launch(clv_sampler* s, int64_t n_sweeps) {
   if (s->d_sums_prev)  // an aborted (or rolled-back) launch restores the running sums from here
     CLV_HIP(hipMemcpyAsync(s->d_sums_prev, s->d_sums, sums_bytes, hipMemcpyDeviceToDevice, s->stream));
   SweepArgs a = sweep_args(s, 0, 1);
+  const int64_t stride_c = (int64_t)g.n_chains * g.stride;
+  a.pend_in = s->pend ? s->d_pend + s->pend_buf * stride_c : nullptr;
+  a.pend_out = s->defer ? s->d_pend + (s->pend_buf ^ 1) * stride_c : nullptr;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (s->timing) {
     int rc = ensure_events(s);
@@ -986,13 +1000,45 @@ int clv::persist_wait(clv_sampler* s) {
   }
   std::swap(s->d_lam, s->d_lam_alt);
   std::swap(s->d_mu, s->d_mu_alt);
-  std::swap(s->d_hyper, s->d_hyper_alt);
+  s->rb_pend = s->pend;  // (rollback: the hyper state this launch started from)
+  s->rb_pend_buf = s->pend_buf;
+  s->rb_hyper_swaps = 0;
+  if (s->defer) {  // the launch's last draw is pending in the other buffer; hyper untouched
+    s->pend = true;
+    s->pend_buf ^= 1;
+  } else {
+    std::swap(s->d_hyper, s->d_hyper_alt);
+    s->rb_hyper_swaps = 1;
+    s->pend = false;
+  }
   if (s->graph_exec) {  // captured with the previous state pointers
     CLV_HIP(hipGraphExecDestroy(s->graph_exec));
     s->graph_exec = nullptr;
   }
   s->sweeps_done += n_sweeps;
   s->last_persist_n = n_sweeps;
+  return CLV_OK;
+}
+
+// The pending level-2 draw of the last launch's last sweep (CLV_DEFER), into hyper (and the
+// level-2 record it belongs to): before anything reads the hyper state or the level-2 records, or
+// runs a sweep that is not a persistent launch.  The same draw (statistics, variates, order) the
+// next launch would make first, so results do not depend on where a run is cut into clv_run calls.
+int clv::persist_flush(clv_sampler* s) {
+  if (!s->pend) return CLV_OK;
+  CLV_HIP(hipSetDevice(s->device));
+  SweepArgs a = sweep_args(s, 0, 1);
+  a.pend_in = s->d_pend + s->pend_buf * (int64_t)s->g.n_chains * s->g.stride;
+  a.pend_out = nullptr;
+  CLV_HIP(launch_persist_flush(a, s->sweeps_done + 1, s->stream));
+  CLV_HIP(hipStreamSynchronize(s->stream));
+  std::swap(s->d_hyper, s->d_hyper_alt);
+  s->rb_hyper_swaps++;
+  s->pend = false;
+  if (s->graph_exec) {
+    CLV_HIP(hipGraphExecDestroy(s->graph_exec));
+    s->graph_exec = nullptr;
+  }
   return CLV_OK;
 }
 
@@ -1125,7 +1171,12 @@ int clv_rollback(clv_sampler* s) {
   CLV_HIP(hipStreamSynchronize(s->stream));
   std::swap(s->d_lam, s->d_lam_alt);
   std::swap(s->d_mu, s->d_mu_alt);
-  std::swap(s->d_hyper, s->d_hyper_alt);
+  // the hyper state the launch started from: pending statistics (still in their buffer), or the
+  // hyper buffer that was current then (in hyper_alt after an odd number of swaps since)
+  if (s->rb_hyper_swaps & 1) std::swap(s->d_hyper, s->d_hyper_alt);
+  s->pend = s->rb_pend;
+  s->pend_buf = s->rb_pend_buf;
+  s->rb_hyper_swaps = 0;
   s->sweeps_done -= s->last_persist_n;
   s->last_persist_n = 0;
   Ctrl c{};
@@ -1145,6 +1196,10 @@ int clv_read_draws(clv_sampler* s, double* level1, double* level2, double* logli
   if (!s) return fail(CLV_EINVAL, "null sampler");
   CLV_HIP(hipSetDevice(s->device));
   CLV_HIP(hipStreamSynchronize(s->stream));
+  if (level2) {
+    int rc = persist_flush(s);  // the last level-2 record may still be pending
+    if (rc) return rc;
+  }
   const Geometry& g = s->g;
   const size_t C = g.n_chains;
   if (level1) {
@@ -1180,6 +1235,10 @@ int clv_get_state(clv_sampler* s, double* lambdas, double* mus, double* hyper) {
   if (!s) return fail(CLV_EINVAL, "null sampler");
   CLV_HIP(hipSetDevice(s->device));
   CLV_HIP(hipStreamSynchronize(s->stream));
+  if (hyper) {
+    int rc = persist_flush(s);
+    if (rc) return rc;
+  }
   const Geometry& g = s->g;
   if (lambdas && g.n) CLV_HIP(hipMemcpy(lambdas, s->d_lam, sizeof(double) * g.n_chains * g.n, hipMemcpyDeviceToHost));
   if (mus && g.n) CLV_HIP(hipMemcpy(mus, s->d_mu, sizeof(double) * g.n_chains * g.n, hipMemcpyDeviceToHost));
@@ -1207,6 +1266,10 @@ int clv_set_state(clv_sampler* s, const double* lambdas, const double* mus, cons
         if (!(v[i] >= 2.2250738585072014e-308 && v[i] <= 1.7976931348623157e308))
           return fail(CLV_EINVAL, "lambdas and mus must be positive, normal and finite");
   CLV_HIP(hipSetDevice(s->device));
+  {  // a pending draw belongs to the state being replaced (its level-2 record too)
+    int rc = persist_flush(s);
+    if (rc) return rc;
+  }
   if (lambdas && g.n) CLV_HIP(hipMemcpy(s->d_lam, lambdas, sizeof(double) * g.n_chains * g.n, hipMemcpyHostToDevice));
   if (mus && g.n) CLV_HIP(hipMemcpy(s->d_mu, mus, sizeof(double) * g.n_chains * g.n, hipMemcpyHostToDevice));
   if (hyper) {

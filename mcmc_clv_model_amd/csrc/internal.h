@@ -17,6 +17,7 @@ int fail(int code, const std::string& msg);
 // its carried state (or restore the state it started from, if a wait in it timed out).
 int persist_launch(clv_sampler* s, int64_t n_sweeps);
 int persist_wait(clv_sampler* s);
+int persist_flush(clv_sampler* s);  // the deferred level-2 draw, if one is pending (synchronous)
 // A persistent grid of grid_wgs workgroups fits at once (with a residency margin) on n_cu CUs
 // admitting blocks_per_cu of its workgroups each (capi.hip).
 bool persist_grid_fits(int64_t grid_wgs, int blocks_per_cu, int n_cu);
@@ -94,6 +95,19 @@ struct clv_sampler {
   bool slots_dirty = true;          // persistent hand-off slots need the sentinel fill (a completed
                                     // launch leaves them empty; only an aborted one does not)
   int64_t last_persist_n = 0;       // sweeps of the last persistent launch (rollback), 0 = none
+  // Deferred level-2 draw (world size 1, persistent, CLV_DEFER != "0"): a launch leaves the draw
+  // that follows its last sweep to the next launch, which draws it first while its customer
+  // workgroups load (kernels.hip persist_level2, iteration -1), or to persist_flush before anything
+  // reads the hyper state or the level-2 records.  The pending statistics live in d_pend[pend_buf]
+  // ([2][chain][stride]: a launch reads one buffer and writes the other, so an aborted launch or a
+  // rollback finds the state it started from intact).
+  bool defer = false;
+  bool pend = false;                // the hyper state is the draw of d_pend[pend_buf], not d_hyper
+  int pend_buf = 0;
+  double* d_pend = nullptr;
+  bool rb_pend = false;             // rollback: the pending state before the last persistent launch
+  int rb_pend_buf = 0;
+  int rb_hyper_swaps = 0;           // hyper / hyper_alt swaps since it (its hyper is in hyper_alt if odd)
   bool persistent = false;          // clv_run uses persist_kernel (all workgroups resident)
   int persist_bpc = 0, n_cu = 0;    // persist_kernel occupancy (workgroups per CU), CUs
   // world size > 1: persistent kernel with the peer (xGMI) exchange

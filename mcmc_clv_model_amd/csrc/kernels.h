@@ -128,6 +128,13 @@ struct SweepArgs {
   double* lam_out;
   double* mu_out;
   double* hyper_out;
+  // persistent kernel, world size 1 (clv_create CLV_DEFER): the level-2 draw that follows a
+  // launch's last sweep is deferred to the next launch (or a flush).  pend_out: the last sweep's
+  // fixed-order statistics [chain][stride] go here instead of being drawn from; pend_in: such
+  // statistics of the sweep before s_first, drawn from first (while the customer workgroups load
+  // and draw their first sweep's variates).  Null: no deferral on that side.
+  const double* pend_in;
+  double* pend_out;
   uint64_t wait_ticks;
   uint32_t* abort_host;
   HyperArgs h;               // level-2 arguments of the fused tail
@@ -148,6 +155,8 @@ hipError_t launch_group(const GroupArgs& a, hipStream_t st);
 hipError_t launch_persist(const SweepArgs& a, int64_t s_first, int64_t n_sweeps, hipStream_t st,
                           hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 hipError_t persist_occupancy(int D, int K, bool p2p, int* blocks_per_cu);
+// The deferred level-2 draw alone (a.pend_in, no sweeps): one level-2 workgroup per chain.
+hipError_t launch_persist_flush(const SweepArgs& a, int64_t s_first, hipStream_t st);
 hipError_t launch_hyper(const HyperArgs& a, bool replay, hipStream_t st);
 hipError_t launch_set_hyper(int D, int K, int n_chains, double* hyper, const double* beta_sigma,
                             double omega2, hipStream_t st);

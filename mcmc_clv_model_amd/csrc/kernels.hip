@@ -1914,7 +1914,13 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
   // waves take issue priority over theirs (it mostly sleeps in polls otherwise).
   __builtin_amdgcn_s_setprio(3);
   stage_prior(a.h.V, &l2);
-  for (int64_t it = 0; it < n_sweeps; ++it) {
+  // deferred draws (world size 1): pin = the statistics of sweep s_first - 1 whose draw the
+  // previous launch left to this one (iteration -1: no poll, drawn while the customer workgroups
+  // load and draw their first variates); pout = where the last sweep's statistics go instead of
+  // being drawn from (the next launch's, or a flush's, iteration -1)
+  const double* pin = P2P ? nullptr : a.pend_in;
+  double* pout = P2P ? nullptr : a.pend_out;
+  for (int64_t it = pin ? -1 : 0; it < n_sweeps; ++it) {
     // the lane's addresses and unit bookkeeping are recomputed every sweep from an opaque copy of
     // the lane index (a few integer ops), not kept live across the loop: registers for the phases
     int tid = tid0;
@@ -1927,14 +1933,20 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
     const bool stp = tid == 0 && it == it_stamp;
     (void)stp;
     const int64_t hs = (D == 2) ? s + 1 : s;  // sweep the drawn (beta, Sigma) belongs to
+    const bool from_pend = it < 0;                           // (uniform)
+    const bool defer_now = pout && it == n_sweeps - 1;       // (uniform) this sweep's draw is deferred
     CLV_P_STAMP(a.stamps, wgi, 0, stp);
     // 1. this draw's variates (as hyper_body without precomputed ones): overlap the sweep
-    if (tid < NTRIL) var_iw[tid] = hyper_normal(k0, k1, HSLOT_NORMAL0 + tid, (uint32_t)hs);
-    if (tid >= 32 && tid < 32 + D * K) var_noise[tid - 32] = hyper_normal(k0, k1, HSLOT_BETA_NORMAL0 + (tid - 32), (uint32_t)hs);
-    if (tid >= 64 && tid < 64 + D) var_chi[tid - 64] = chi2_draw(k0, k1, (uint32_t)hs, tid - 64, a.h.nu_n - D + 1 + (tid - 64));
+    if (!defer_now) {
+      if (tid < NTRIL) var_iw[tid] = hyper_normal(k0, k1, HSLOT_NORMAL0 + tid, (uint32_t)hs);
+      if (tid >= 32 && tid < 32 + D * K) var_noise[tid - 32] = hyper_normal(k0, k1, HSLOT_BETA_NORMAL0 + (tid - 32), (uint32_t)hs);
+      if (tid >= 64 && tid < 64 + D) var_chi[tid - 64] = chi2_draw(k0, k1, (uint32_t)hs, tid - 64, a.h.nu_n - D + 1 + (tid - 64));
+    }
+    if (from_pend && tid < NS) tot[tid] = pin[(int64_t)c * NS + tid];  // the fixed-order sums, as stored
     __syncthreads();
-    if (tid == 0) bartlett_inverse<D>(var_iw, var_chi, l2.Ai);  // read back by this lane only
+    if (!defer_now && tid == 0) bartlett_inverse<D>(var_iw, var_chi, l2.Ai);  // read back by this lane only
     CLV_P_STAMP(a.stamps, wgi, 1, stp);
+    if (!from_pend) {
     // 2. wait for every block partial of sweep s (lane tid: blocks tid, tid + NT; nb <= 2 NT).
     //    The persistent kernel's partials are [block][stat]: one base address per block and the
     //    statistics at immediate offsets (no per-statistic 64-bit addresses held across the poll).
@@ -2095,13 +2107,14 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
     block_reduce<NS, NT, P2P>(acc, red, tot);  // also publishes the variates (LDS)
     CLV_P_STAMP(a.stamps, wgi, 6, stp);
     // 4. reset: the partial slots (their writers write again only after step 6) and the
-    //    (beta, Sigma) set every reader of s has read (its next write is for s+2)
+    //    (beta, Sigma) set every reader of s has read (its next write is for s+2; at sweep s_first
+    //    of a launch that drew a deferred draw first, its readers took it from this slot too)
 #pragma unroll
     for (int j = 0; j < NS; ++j) {
       if (hb0) st_wt(pb0 + j, slot_empty());
       if (hb1) st_wt(pb1 + j, slot_empty());
     }
-    if (it > 0 && tid < HS) st_wt(a.hyp2 + ((int64_t)(s & 1) * g.n_chains + c) * HS + tid, slot_empty());
+    if ((it > 0 || pin) && tid < HS) st_wt(a.hyp2 + ((int64_t)(s & 1) * g.n_chains + c) * HS + tid, slot_empty());
     if constexpr (P2P) {  // this rank's mail slots of sweep s: empty again before any rank can
                           // write sweep s + 2 there (only after this rank's units of s + 1, which
                           // leave after the vmcnt(0) below)
@@ -2110,6 +2123,16 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
         if (m0) st_sys((double*)p0 + j, slot_empty());
         if (m1) st_sys((double*)p1 + j, slot_empty());
       }
+    }
+    }  // (!from_pend)
+    if (defer_now) {  // the last sweep's statistics to the next launch (kernel boundary: plain
+                      // stores), its log-likelihood record now; the slots above are empty again
+      if (tid < NS) pout[(int64_t)c * NS + tid] = tot[tid];
+      if (tid == 0) {
+        if (is_stored(s, g)) a.h.loglik[(int64_t)c * g.n_draws + draw_index(s, g)] = tot[NS - 1] / (double)g.n_global;
+        a.ctrl_rw->cur = s;
+      }
+      return;
     }
     if (tid < HS) Hs[tid] = 0.0;  // unwritten hyper slots publish as 0 (wavefront 0: ordered before the draw's writes)
     // 5. the draw (wavefront 0) while the resets drain
@@ -2152,7 +2175,8 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
 #pragma unroll
           for (int r = p; r < D; ++r) o[q++] = l2.Sig[p * D + r];  // bi:412, tri:550-554
       }
-      if (is_stored(s, g)) a.h.loglik[(int64_t)c * g.n_draws + draw_index(s, g)] = tot[NS - 1] / (double)g.n_global;
+      // (a deferred draw's log-likelihood record was written by the launch that deferred it)
+      if (!from_pend && is_stored(s, g)) a.h.loglik[(int64_t)c * g.n_draws + draw_index(s, g)] = tot[NS - 1] / (double)g.n_global;
       if (last) a.ctrl_rw->cur = s;
     }
     __syncthreads();  // LDS (tot, l2, Hs, variates) reused next sweep
@@ -2334,7 +2358,7 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
     CLV_P_STAMP(a.stamps, wgi, 0, stp);
     // consumer: this sweep's first MH-variate chunks from the producers (drawn during sweep s - 1)
     if (pc_off > 0 && it > 0 && pre && !pc_consume(a, pc_off, s, T_wg, L_wg, pv)) s_abort = 1;
-    if (it > 0) {  // wait for (beta, Sigma) of sweep s (wavefront 0 polls, one slot per lane)
+    if (it > 0 || (!P2P && a.pend_in)) {  // wait for (beta, Sigma) of sweep s (wavefront 0 polls, one slot per lane)
       if (tid < 64) {
         const double* src = hyp_c + (int64_t)(s & 1) * g.n_chains * HS;
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -2411,6 +2435,18 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
     a.lam_out[ci] = cu.lam;
     a.mu_out[ci] = cu.mu;
   }
+}
+
+// The deferred level-2 draw alone (clv_run's flush before anything reads the hyper state or the
+// level-2 records): persist_level2's iteration -1 with no sweeps, one workgroup per chain; it
+// writes hyper_out, the level-2 record and ctrl->cur as the end of a launch does.
+template <int D, int K>
+__global__ __launch_bounds__(BLOCK) void persist_flush_kernel(SweepArgs a, int64_t s_first) {
+  __shared__ double pool[1];
+  const int c = blockIdx.y;
+  uint32_t k0, k1;
+  chain_key(a.r.seed, (int64_t)a.r.chain_first + c, &k0, &k1);
+  persist_level2<D, K, false>(a, s_first, 0, c, k0, k1, 0, -2, pool);
 }
 
 // (beta, Sigma) -> hyper state for every chain: [chain][K*D + D*D] input.
@@ -2591,6 +2627,19 @@ hipError_t launch_sweep(const SweepArgs& a, bool replay, hipStream_t st, hipEven
   CLV_FOR_K(CLV_CASE, 3, false)
   CLV_FOR_K(CLV_CASE, 2, true)
   CLV_FOR_K(CLV_CASE, 3, true)
+#undef CLV_CASE
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_persist_flush(const SweepArgs& a, int64_t s_first, hipStream_t st) {
+  const dim3 grid(1, a.g.n_chains);
+#define CLV_CASE(DD, KK, PP)                                                                     \
+  if (a.g.D == DD && a.g.K == KK) {                                                              \
+    hipLaunchKernelGGL((persist_flush_kernel<DD, KK>), grid, dim3(BLOCK), 0, st, a, s_first);  \
+    return hipGetLastError();                                                                  \
+  }
+  CLV_FOR_K(CLV_CASE, 2, false)
+  CLV_FOR_K(CLV_CASE, 3, false)
 #undef CLV_CASE
   return hipErrorInvalidValue;
 }

@@ -569,6 +569,71 @@ def test_persistent_kernel_bitwise_equals_launch_per_sweep(L, monkeypatch, D, co
             assert np.array_equal(bits(x), bits(y))
 
 
+def _run_ops(p, env, ops, **kw):
+    """A sampler created under `env`, driven by `ops` ("run", n) / ("state",) / ("rollback",);
+    returns the states taken at ("state",) ops, the final state and the draws."""
+    from mcmc_clv_model_amd.sampler import HipSampler
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        s = HipSampler(p, **kw)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+    mid = []
+    with s:
+        info = s.launch_info()
+        for op in ops:
+            if op[0] == "run":
+                s.run(op[1])
+            elif op[0] == "state":
+                mid.append(s.get_state())
+            else:
+                s.rollback()
+        st = s.get_state()
+        l1, l2, ll = s.read_draws(level1=kw.get("draw_sink", "full") == "full")
+        sums = s.read_summary()[0] if kw.get("draw_sink") in ("summary", "summary+pct") else None
+    return info, mid, st, l1, l2, ll, sums
+
+
+def _same_bits(a, b):
+    for x, y in zip(a, b):
+        if isinstance(x, (list, tuple)):
+            _same_bits(x, y)
+        elif x is not None:
+            assert np.array_equal(bits(x), bits(y))
+
+
+@pytest.mark.parametrize("D,covs,sink", [(2, ["first_sales_scaled"], "full"), (3, ["gender_F", "age_scaled"], "summary")])
+def test_deferred_level2_draw_bitwise(L, D, covs, sink):
+    """Verdict r3 #1: a persistent launch leaves the level-2 draw after its last sweep to the next
+    launch (drawn first, while the customer workgroups load) or to a flush before anything reads
+    the hyper state or the level-2 records.  Bit for bit the same run as without deferral
+    (CLV_DEFER=0) and as the launch-per-sweep path, over uneven clv_run calls including 1-sweep
+    calls, with get_state between calls (a flush mid-run), and through clv_rollback at world size 1
+    (undo a completed call and redo it; also after a flush)."""
+    from mcmc_clv_model_amd.sampler import build_problem
+    p = build_problem(cdnow("full", 23570), covs, D)
+    kw = dict(mcmc=22, burnin=5, thin=2, chains=2, seed=77, draw_sink=sink)
+    ops = [("run", 1), ("run", 1), ("run", 6), ("state",), ("run", 3), ("run", 1), ("state",), ("run", 15)]
+    ref = _run_ops(p, {"CLV_PERSISTENT": "0"}, ops, **kw)
+    nodef = _run_ops(p, {"CLV_PERSISTENT": "1", "CLV_DEFER": "0"}, ops, **kw)
+    dfr = _run_ops(p, {"CLV_PERSISTENT": "1", "CLV_DEFER": "1"}, ops, **kw)
+    assert not ref[0]["persistent"] and nodef[0]["persistent"] and dfr[0]["persistent"]
+    _same_bits(ref[1:], nodef[1:])
+    _same_bits(ref[1:], dfr[1:])
+    # rollback of a deferred call (pending draw in, pending draw out), and after a flush
+    rb = [("run", 4), ("run", 5), ("rollback",), ("run", 5), ("run", 3), ("state",), ("rollback",), ("run", 3),
+          ("run", 15)]
+    straight = [("run", 4), ("run", 5), ("run", 3), ("state",), ("run", 15)]
+    a = _run_ops(p, {"CLV_PERSISTENT": "1", "CLV_DEFER": "1"}, rb, **kw)
+    b = _run_ops(p, {"CLV_PERSISTENT": "1", "CLV_DEFER": "1"}, straight, **kw)
+    _same_bits(a[1:], b[1:])
+
+
 @pytest.mark.parametrize("chunks", ["0", "1", "2"])
 def test_producer_consumer_variates_bitwise(L, monkeypatch, chunks):
     """c2's layout (4 chains x 23,570 customers: 376 workgroups on 256 CUs): consumer workgroups on
