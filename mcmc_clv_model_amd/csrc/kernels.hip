@@ -1507,6 +1507,9 @@ static_assert(BLOCK == EXP_TAB_N, "the sweep kernel stages the exp table with on
 // FX: the fused peer exchange (world size > 1 after clv_p2p_connect) compiled in — instances of
 // their own, launched for sharded runs only (compiled into the world-size-1 kernels it cost c4 /
 // c5 1.8% / 1.6% per sweep).
+#ifndef CLV_TAIL_STORE_LATE
+#define CLV_TAIL_STORE_LATE 1
+#endif
 template <int D, int K, bool REPLAY, bool FX>
 __device__ __forceinline__ void sweep_body(const SweepArgs& a) {
   constexpr int NT = BLOCK;
@@ -1763,7 +1766,12 @@ __device__ __forceinline__ void sweep_body(const SweepArgs& a) {
     }
     __syncthreads();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only
-    finish_store();
+    // the chain's last unit stores after its level-2 draw: the draw's loads would otherwise wait
+    // (vmcnt counts in order) for the sums' and draws' stores, on every sweep's serial tail
+    // (bivariate instances: the trivariate ones would hold the stores' operands across the draw at
+    // 149 instead of 125 VGPRs, 3 instead of 4 waves per SIMD)
+    constexpr bool LATE = CLV_TAIL_STORE_LATE && D == 2;
+    if (!LATE || !s_last) finish_store();
     if (s_last) {
       if (threadIdx.x == 0) CLV_STAMP(a.stamps, s, 2, false);
       if (!fx) {
@@ -1827,6 +1835,7 @@ __device__ __forceinline__ void sweep_body(const SweepArgs& a) {
         }
       }
       if (threadIdx.x == 0) CLV_STAMP(a.stamps, s, 3, false);
+      if (LATE) finish_store();
     }
   }
 }
