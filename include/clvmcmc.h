@@ -274,6 +274,12 @@ int clv_debug_wg_map(int32_t n_chains, int32_t nb, int32_t n_cu, int32_t* out);
  * admitting blocks_per_cu of them each: min(blocks_per_cu, 8, the SGPR rule at 102 SGPRs) per CU,
  * less one slot per 32 CUs (MI355X guide, residency of 256-thread blocks), else 0. */
 int clv_debug_persist_fits(int64_t grid_wgs, int32_t blocks_per_cu, int32_t n_cu);
+/* Host only: 1 if clv_create runs a grid of grid_wgs persistent workgroups (n_chains chains of a
+ * D / K model) on n_cu CUs: it fits (clv_debug_persist_fits) and few enough CUs hold two of its
+ * workgroups for it to beat the launch-per-sweep kernel (capi.hip persist_worth, measured
+ * crossover); CLV_PERSISTENT=1 forces it wherever it fits, =0 never. */
+int clv_debug_persist_choice(int32_t D, int32_t K, int32_t n_chains, int64_t grid_wgs, int32_t blocks_per_cu,
+                             int32_t n_cu);
 /* Host only: the persistent grid's MH-variate producer / consumer roles for n_chains chains of nb
  * customer workgroups on n_cu CUs with up to n_off chunks per consumer and at most load_x100 / 100
  * tasks per producer on average (0: no cap) — out[linear workgroup][8]: [0] chunks taken from

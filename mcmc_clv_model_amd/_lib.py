@@ -123,6 +123,7 @@ def lib() -> ctypes.CDLL:
         "clv_debug_mh_step": (c_int32, [c_int64, POINTER(c_int32), POINTER(c_uint8), dp, dp, dp, dp, dp,
                                         POINTER(c_float), dp, POINTER(c_float), dp]),
         "clv_debug_wg_map": (c_int32, [c_int32, c_int32, c_int32, POINTER(c_int32)]),
+        "clv_debug_persist_choice": (c_int32, [c_int32, c_int32, c_int32, c_int64, c_int32, c_int32]),
         "clv_debug_persist_fits": (c_int32, [c_int64, c_int32, c_int32]),
         "clv_debug_pc_plan": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_int32, POINTER(c_int32)]),
         "clv_group_create": (c_int32, [POINTER(sp), c_int32, c_int32, POINTER(sp)]),

@@ -251,6 +251,23 @@ bool clv::persist_grid_fits(int64_t grid_wgs, int blocks_per_cu, int n_cu) {
   return grid_wgs > 0 && slots > 0 && grid_wgs <= slots - margin;
 }
 
+// Whether the persistent kernel is worth running a resident grid of grid_wgs workgroups (world size
+// 1 and the peer exchange): it holds every customer's state in registers and pays no launch per
+// sweep, but all its customer waves stay resident, so once most CUs hold two workgroups the
+// doubled SIMDs (two waves each, issue-bound) set every sweep's period, where the launch-per-sweep
+// kernel runs 4 waves per SIMD and load-balances.  Measured crossover (tools/persist_crossover.py,
+// profiles/r04_persist_crossover*.jsonl; us per sweep persistent / launch-per-sweep): bivariate
+// K=2, 4 chains: 1.25 workgroups per CU 10.9 / 17.6, 1.61 12.6 / 18.7, 1.86 19.6 / 19.5; K=5,
+// 1 chain: 0.92 12.5 / 17.3, 1.38 21.0 / 20.8, 1.68 31.9 / 21.8, 1.91 43.8 / 22.4 (c4 at 8 ranks);
+// trivariate K=3, 4 chains: 1.25 12.5 / 20.3, 1.61 12.8 / 21.5.
+bool clv::persist_worth(int D, int K, int n_chains, int64_t grid_wgs, int n_cu) {
+  (void)D;
+  (void)K;
+  if (n_cu <= 0) return false;
+  const double per_cu = (double)grid_wgs / n_cu;
+  return per_cu <= (n_chains >= 2 ? 1.65 : 1.35);
+}
+
 namespace {
 
 // Persistent grid: which (chain, block) each dispatched workgroup runs.  The grid has more
@@ -478,7 +495,11 @@ int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* pri
     if (persist_occupancy(g.D, g.K, false, &s->persist_bpc) == hipSuccess &&
         hipGetDeviceProperties(&prop, s->device) == hipSuccess)
       s->n_cu = prop.multiProcessorCount;
-    if ((!env || std::string(env) != "0") && persist_grid_fits((int64_t)(nb_local + 1) * C, s->persist_bpc, s->n_cu))
+    // CLV_PERSISTENT: "0" never, "1" whenever the grid fits (tests, A/B), unset: where it pays
+    const int64_t grid = (int64_t)(nb_local + 1) * C;
+    const bool force = env && std::string(env) == "1";
+    if ((!env || std::string(env) != "0") && persist_grid_fits(grid, s->persist_bpc, s->n_cu) &&
+        (force || persist_worth(g.D, g.K, (int)C, grid, s->n_cu)))
       s->persistent = true;
   }
   // World size > 1: the same persistent kernel exchanging unit partials with its peers over xGMI
@@ -491,7 +512,10 @@ int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* pri
         hipGetDeviceProperties(&prop, s->device) == hipSuccess)
       s->n_cu = prop.multiProcessorCount;
     const char* env = std::getenv("CLV_PERSISTENT");  // "0": the fused exchange below instead
-    if ((!env || std::string(env) != "0") && persist_grid_fits((int64_t)(nb_local + 1) * C, s->persist_bpc, s->n_cu))
+    const int64_t grid = (int64_t)(nb_local + 1) * C;
+    const bool force = env && std::string(env) == "1";
+    if ((!env || std::string(env) != "0") && persist_grid_fits(grid, s->persist_bpc, s->n_cu) &&
+        (force || persist_worth(g.D, g.K, (int)C, grid, s->n_cu)))
       s->p2p_capable = true;
   }
   // Any other shard: the sweep kernel's fused level-2 tail exchanges through the same mail (one
@@ -1447,6 +1471,11 @@ int clv_debug_pc_plan(int32_t n_chains, int32_t nb, int32_t n_cu, int32_t n_off,
   if (d.empty()) std::fill(out, out + T * PC_DESC, 0);
   else std::copy(d.begin(), d.end(), out);
   return CLV_OK;
+}
+
+int clv_debug_persist_choice(int32_t D, int32_t K, int32_t n_chains, int64_t grid_wgs, int32_t blocks_per_cu,
+                             int32_t n_cu) {
+  return persist_grid_fits(grid_wgs, blocks_per_cu, n_cu) && persist_worth(D, K, n_chains, grid_wgs, n_cu) ? 1 : 0;
 }
 
 int clv_debug_persist_fits(int64_t grid_wgs, int32_t blocks_per_cu, int32_t n_cu) {

@@ -21,6 +21,7 @@ int persist_flush(clv_sampler* s);  // the deferred level-2 draw, if one is pend
 // A persistent grid of grid_wgs workgroups fits at once (with a residency margin) on n_cu CUs
 // admitting blocks_per_cu of its workgroups each (capi.hip).
 bool persist_grid_fits(int64_t grid_wgs, int blocks_per_cu, int n_cu);
+bool persist_worth(int D, int K, int n_chains, int64_t grid_wgs, int n_cu);
 
 template <class T>
 hipError_t dalloc(T** p, size_t count) {

@@ -93,6 +93,28 @@ def test_persistent_residency_margin():
     assert fits(6 * 256 - 8, 7) and not fits(6 * 256 - 7, 7)  # the SGPR term caps 7 / 8 blocks per CU at 6
 
 
+def test_persistent_choice_by_grid_density():
+    """Verdict r3 #8: which grids run the persistent kernel (world size 1, and the peer exchange at
+    world size > 1).  Measured (tools/persist_crossover.py): once most CUs hold two of its
+    workgroups it loses to the launch-per-sweep kernel — c4's 8-rank shard (1 chain, 496 blocks +
+    1 level-2 workgroup = 497 of 504 slots; persist_kernel<2,5,true>, 256 VGPRs) would run ~2x
+    slower than the fused exchange, so it takes the fused exchange; c2 / c3 (4 x 94 = 376), c2 tiled
+    per rank at 8 ranks (the same 376) and c1 keep it."""
+    from mcmc_clv_model_amd import _lib
+    from mcmc_clv_model_amd.distributed import plan
+    L = _lib.lib()
+    pick = lambda D, K, C, wgs, bpc=2: bool(L.clv_debug_persist_choice(D, K, C, wgs, bpc, 256))  # noqa: E731
+    assert pick(2, 2, 4, 4 * (93 + 1)) and pick(3, 3, 4, 4 * (93 + 1))        # c2, c3
+    assert pick(2, 1, 4, 4 * (10 + 1))                                      # c1 (2,357 customers)
+    p8 = plan(1_000_000, 8)
+    nb_rank = -(-(p8.shard(0)[1] - p8.shard(0)[0]) // 256)
+    assert nb_rank == 496 and L.clv_debug_persist_fits(nb_rank + 1, 2, 256)  # it would fit ...
+    assert not pick(2, 5, 1, nb_rank + 1)                                   # ... but is not chosen
+    assert not pick(2, 5, 1, 490) and pick(2, 5, 1, 236)                    # measured: 43.8 vs 22.4 / 12.5 vs 17.3 us
+    assert pick(2, 2, 4, 412) and not pick(2, 2, 4, 476)                    # 12.6 vs 18.7 / 19.6 vs 19.5 us
+    assert not pick(2, 2, 4, 505)                                           # does not fit at all
+
+
 @pytest.mark.parametrize("C,nb,n_off,load", [(4, 93, 3, 0), (3, 93, 3, 0), (4, 93, 5, 0), (2, 200, 2, 0), (8, 40, 1, 0),
                                              (4, 10, 3, 0), (4, 93, 2, 200), (4, 93, 3, 250), (4, 93, 1, 50)])
 def test_producer_consumer_plan(C, nb, n_off, load):
