@@ -127,7 +127,11 @@ int64_t clv_replay_sweep_stride(const clv_sampler* s);
 
 /* Run n sweeps (world_size == 1, or sharded after clv_p2p_connect). One sweep = a6's loop body: z (bi:388),
  * tau (bi:390), level-2 (bi:393), level-1 MH (bi:396), eta (tri:524-526), storage (bi:402-428).
- * Synchronous; chunks of sweeps are replayed from a captured hipGraph. */
+ * Synchronous; chunks of sweeps are replayed from a captured hipGraph.  The persistent path at
+ * world size 1 leaves the level-2 draw that follows its last sweep pending (CLV_DEFER, default on):
+ * the next clv_run draws it first, and clv_get_state / clv_set_state / clv_read_draws (level 2) /
+ * clv_sweep / clv_hyper draw it before they read or replace the state — the same draw either way,
+ * so results never depend on how a run is cut into clv_run calls. */
 int clv_run(clv_sampler* s, int64_t n_sweeps);
 /* Persistent path only: undo the last completed clv_run (state, sweep count, summary sums) — a
  * sharded step whose persistent launch failed on another rank is redone by every rank from the

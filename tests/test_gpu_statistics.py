@@ -135,3 +135,121 @@ def test_published_table3_config1():
     x = cbs["x"].to_numpy()
     total_loglik = float(d["log_likelihood"]) * len(cbs) - gammaln(x + 1).sum()
     assert abs(total_loglik - pub["loglik"]) <= 0.01 * abs(pub["loglik"]), (total_loglik, pub["loglik"])
+
+
+# ---------------------------------------------------------------------------------------------
+# Invariance of the SHIPPED MH step (verdict r3: the production step, not the replay instance)
+def _target_lp(ll, lm, x, z, w, m, P):
+    """bi:291-310 for one customer (K = 1 mean row m, precision P), up to a constant; Q3 cap."""
+    dl, dm = ll - m[0], lm - m[1]
+    with np.errstate(over="ignore", invalid="ignore"):
+        lp = x * ll + (1 - z) * lm - w * (np.exp(ll) + np.exp(lm)) - 0.5 * (P[0, 0] * dl * dl + 2 * P[0, 1] * dl * dm
+                                                                              + P[1, 1] * dm * dm)
+    return np.where(lm > 5.0, -np.inf, lp)
+
+
+def _exact_sample(n, x, z, w, m, P, rng):
+    """n exact draws of the customer's (log lambda, log mu) target by rejection from a wide
+    Student-t(4) envelope around the grid mode (the bound M taken on a fine grid x 1.5)."""
+    g = np.linspace(-16, 8, 1201)
+    LL, LM = np.meshgrid(g, g, indexing="ij")
+    lp = _target_lp(LL, LM, x, z, w, m, P)
+    i = np.unravel_index(np.argmax(lp), lp.shape)
+    mode = np.array([LL[i], LM[i]])
+    prob = np.exp(lp - lp.max())
+    mu = np.array([(prob * LL).sum(), (prob * LM).sum()]) / prob.sum()
+    cov = np.cov(np.stack([LL.ravel(), LM.ravel()]), aweights=prob.ravel())
+    Sc = 4.0 * cov
+    Si = np.linalg.inv(Sc)
+    ldet = np.log(np.linalg.det(Sc))
+
+    def lq(a, b):  # bivariate t(4) log density (up to its constant, consistently)
+        d = np.stack([a - mu[0], b - mu[1]], -1)
+        qf = np.einsum("...i,ij,...j->...", d, Si, d)
+        return -0.5 * ldet - 3.0 * np.log1p(qf / 4.0)
+    logM = np.max(lp - lp.max() - lq(LL, LM)) + np.log(1.5)
+    out = []
+    got = 0
+    Lc = np.linalg.cholesky(Sc)
+    while got < n:
+        k = 4 * (n - got) + 1000
+        y = rng.standard_normal((k, 2)) @ Lc.T / np.sqrt(rng.chisquare(4, (k, 1)) / 4.0) + mu
+        la = _target_lp(y[:, 0], y[:, 1], x, z, w, m, P) - lp.max() - lq(y[:, 0], y[:, 1]) - logM
+        assert np.nanmax(la[np.isfinite(la)]) <= 0.0, "envelope bound violated"
+        acc = np.log(rng.random(k)) < la
+        out.append(y[acc])
+        got += int(acc.sum())
+    return np.concatenate(out)[:n], (LL, LM, prob), mode
+
+
+@pytest.mark.parametrize("case", ["alive", "churned"])
+def test_shipped_mh_step_preserves_the_target(case):
+    """The production MH step (kernels.hip mh_step: fp32 Student-t(3) proposal by the shipped
+    t3_f32 transform, fp32 log2 U, table exp, accept iff pm <= 5 and plp > cur + ln2 log2 U)
+    leaves the reference's level-1 target (bi:291-310) invariant: 1,000,000 exact draws of one
+    customer's (log lambda, log mu) posterior (rejection sampling, numpy) go through 20 steps of the
+    device step with the device's own Philox variates (clv_debug_variates: the sweep kernels' t_l,
+    t_m and accept uniforms); the moments after the steps must equal the target's (grid
+    quadrature) within 5 standard errors.  The same test with the accept threshold shifted by
+    ln 2 * 0.15 (the acceptance ratio scaled by 2^0.15, +11%) must fail it — the test's power (a CPU
+    simulation of this test flags a 2^0.05 bias at 5-7 standard errors, 2^0.02 at 3.5-5)."""
+    import ctypes
+
+    from mcmc_clv_model_amd import _lib
+    L = _lib.lib()
+    rng = np.random.default_rng(31 if case == "alive" else 32)
+    S = np.array([[1.37, 0.33], [0.33, 3.80]])  # Table 3's HB M1 medians (Sigma)
+    P = np.linalg.inv(S)
+    m = np.array([-3.5, -3.7])
+    x, z, T, tau = (3, 1, 39.0, 39.0) if case == "alive" else (5, 0, 39.0, 12.5)
+    w = T if z else tau
+    n, steps = 1_000_000, 20
+    pts, (LL, LM, prob), _ = _exact_sample(n, x, z, w, m, P, rng)
+    pr = prob / prob.sum()
+    exact = dict(ll=(pr * LL).sum(), lm=(pr * LM).sum(), ll2=(pr * LL * LL).sum(), lm2=(pr * LM * LM).sum(),
+                 llm=(pr * LL * LM).sum())
+
+    tl = np.empty((steps, n), np.float32)
+    tm = np.empty((steps, n), np.float32)
+    ua = np.empty((steps, n), np.float32)
+    dummy = [np.empty(n) for _ in range(4)]
+    fp = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))  # noqa: E731
+    dp = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))  # noqa: E731
+    assert L.clv_debug_variates(4242, 0, 7, n, steps, fp(tl), fp(tm), fp(ua), *[dp(d) for d in dummy]) == 0
+    log2u = np.log2(ua)  # fp32, as v_log_f32 of the same uniform (to an fp32 ulp)
+
+    xs = np.full(n, x, np.int32)
+    zs = np.full(n, z, np.uint8)
+    Ts, taus = np.full(n, T), np.full(n, tau)
+    mean = np.ascontiguousarray(np.tile(m, (n, 1)))
+    prec = np.array([P[0, 0], P[0, 1], P[1, 1]])
+    scale = np.array([S[0, 0], S[1, 1]])
+
+    def run(shift):
+        cur = np.ascontiguousarray(pts.copy())
+        out = np.zeros((n, 7))
+        for j in range(steps):
+            t3 = np.ascontiguousarray(np.stack([tl[j], tm[j]], -1))
+            lu = np.ascontiguousarray((log2u[j] + shift).astype(np.float32))
+            assert L.clv_debug_mh_step(n, xs.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                       zs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), dp(Ts), dp(taus), dp(mean),
+                                       dp(prec), dp(cur), fp(t3), dp(scale), fp(lu), dp(out)) == 0
+            cur = np.ascontiguousarray(out[:, 4:6])
+        return cur, float(np.mean(out[:, 4] != pts[:, 0]))
+
+    def zscores(a):
+        ll, lm = a[:, 0], a[:, 1]
+        zs_ = {}
+        for k, v in dict(ll=ll, lm=lm, ll2=ll * ll, lm2=lm * lm, llm=ll * lm).items():
+            zs_[k] = (v.mean() - exact[k]) / (v.std() / np.sqrt(n))
+        return zs_
+
+    z_in = zscores(pts)
+    assert max(abs(v) for v in z_in.values()) < 5, z_in  # the exact sample is exact
+    after, moved = run(0.0)
+    assert moved > 0.3, moved  # the chain moves
+    z_out = zscores(after)
+    assert max(abs(v) for v in z_out.values()) < 5, z_out
+    biased, _ = run(-0.15)  # accept ratio x 2^0.15: must be detected
+    z_b = zscores(biased)
+    assert max(abs(v) for v in z_b.values()) > 5, z_b
