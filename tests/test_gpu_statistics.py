@@ -186,7 +186,7 @@ def _exact_sample(n, x, z, w, m, P, rng):
 def test_shipped_mh_step_preserves_the_target(case):
     """The production MH step (kernels.hip mh_step: fp32 Student-t(3) proposal by the shipped
     t3_f32 transform, fp32 log2 U, table exp, accept iff pm <= 5 and plp > cur + ln2 log2 U)
-    leaves the reference's level-1 target (bi:291-310) invariant: 1,000,000 exact draws of one
+    leaves the reference's level-1 target (bi:291-310) invariant: 400,000 exact draws of one
     customer's (log lambda, log mu) posterior (rejection sampling, numpy) go through 20 steps of the
     device step with the device's own Philox variates (clv_debug_variates: the sweep kernels' t_l,
     t_m and accept uniforms); the moments after the steps must equal the target's (grid
@@ -203,7 +203,7 @@ def test_shipped_mh_step_preserves_the_target(case):
     m = np.array([-3.5, -3.7])
     x, z, T, tau = (3, 1, 39.0, 39.0) if case == "alive" else (5, 0, 39.0, 12.5)
     w = T if z else tau
-    n, steps = 1_000_000, 20
+    n, steps = 400_000, 20
     pts, (LL, LM, prob), _ = _exact_sample(n, x, z, w, m, P, rng)
     pr = prob / prob.sum()
     exact = dict(ll=(pr * LL).sum(), lm=(pr * LM).sum(), ll2=(pr * LL * LL).sum(), lm2=(pr * LM * LM).sum(),
