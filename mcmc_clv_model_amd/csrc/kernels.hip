@@ -2207,7 +2207,8 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
 // finite floats): the consumer polls until its words are there, copies them to its LDS pool and
 // empties the slots.  Slot reuse (sweep s + 2) follows the level-2 hand-off: a producer writes
 // them only after (beta, Sigma) of s + 1, published after the consumer's partial of s, which
-// leaves after its resets (write-through stores, waited for before the partial).
+// leaves after its resets (write-through stores, each wave waiting for its own right after
+// pc_consume, before the (beta, Sigma) wait).
 __device__ __forceinline__ double pack_f2(float lo, float hi) {
   return bitsd((uint64_t)__float_as_uint(lo) | ((uint64_t)__float_as_uint(hi) << 32));
 }
@@ -2366,7 +2367,13 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
     (void)stp;
     CLV_P_STAMP(a.stamps, wgi, 0, stp);
     // consumer: this sweep's first MH-variate chunks from the producers (drawn during sweep s - 1)
-    if (pc_off > 0 && it > 0 && pre && !pc_consume(a, pc_off, s, T_wg, L_wg, pv)) s_abort = 1;
+    if (pc_off > 0 && it > 0 && pre) {
+      if (!pc_consume(a, pc_off, s, T_wg, L_wg, pv)) s_abort = 1;
+      // the slot resets (every wave's own write-through stores) complete before this sweep's partial
+      // can leave, so a producer's store for sweep s + 2 never meets a reset still in flight (ADVICE
+      // r3: the ordering the slot reuse relies on, made explicit; it overlaps the (beta, Sigma) wait)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     if (it > 0 || (!P2P && a.pend_in)) {  // wait for (beta, Sigma) of sweep s (wavefront 0 polls, one slot per lane)
       if (tid < 64) {
         const double* src = hyp_c + (int64_t)(s & 1) * g.n_chains * HS;
