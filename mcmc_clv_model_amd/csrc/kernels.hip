@@ -1847,8 +1847,11 @@ template <int D, int K, bool REPLAY, bool FX>
 __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
   sweep_body<D, K, REPLAY, FX>(a);
 }
+#ifndef SWEEP_OCC_WAVES  // (A/B builds: the occupancy target of the occ4 instances)
+#define SWEEP_OCC_WAVES 4
+#endif
 template <int D, int K, bool REPLAY, bool FX>
-__global__ __launch_bounds__(BLOCK, 4) void sweep_kernel_occ4(SweepArgs a) {
+__global__ __launch_bounds__(BLOCK, SWEEP_OCC_WAVES) void sweep_kernel_occ4(SweepArgs a) {
   sweep_body<D, K, REPLAY, FX>(a);
 }
 
