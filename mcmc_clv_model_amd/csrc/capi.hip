@@ -1135,6 +1135,8 @@ int run_fused_exchange(clv_sampler* s, int64_t n_sweeps) {
   const bool aborted = __atomic_load_n(s->h_abort, __ATOMIC_ACQUIRE) != 0;
   if (rc == CLV_OK && !aborted) {
     s->last_persist_n = n_sweeps;
+    s->rb_pend = false;      // (rollback: the hyper state before the call is the copy in hyper_alt)
+    s->rb_hyper_swaps = 1;
     return CLV_OK;
   }
   // back to the state before the call (copies: a captured graph keeps the buffer addresses)
