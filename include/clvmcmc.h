@@ -153,12 +153,12 @@ int clv_copy_partials(clv_sampler* s, void* dst_device_ptr);
 int clv_synchronize(clv_sampler* s);
 int64_t clv_sweeps_done(const clv_sampler* s);
 /* How clv_run launches: out[6] = (persistent 0/1, persistent-kernel workgroups per CU, CUs,
- * workgroups per sweep, MH-variate chunks each consumer workgroup takes from producer workgroups
- * (0: no producer / consumer split; CLV_PC_CHUNKS), reserved (0)).
+ * workgroups per sweep, reserved (0), reserved (0)).
  * Persistent = one launch for all of a clv_run's sweeps with every customer block resident, chosen
  * at create when world_size == 1, Philox mode, every workgroup fits at once (with a residency
- * margin), and CLV_PERSISTENT != "0".  Otherwise one launch of the sweep kernel per sweep (fused
- * level-2 tail), replayed from captured hipGraph chunks. */
+ * margin) and few enough CUs hold two of them for it to pay (clv_debug_persist_choice), unless
+ * CLV_PERSISTENT is "0" ("1": wherever it fits).  Otherwise one launch of the sweep kernel per
+ * sweep (fused level-2 tail), replayed from captured hipGraph chunks. */
 int clv_launch_info(const clv_sampler* s, int64_t* out);
 /* Sharded runs without a host collective per sweep (world_size > 1, Philox mode): the persistent
  * kernel's level-2 workgroup of each chain writes this rank's unit partials of sweep s straight into
@@ -284,12 +284,6 @@ int clv_debug_persist_fits(int64_t grid_wgs, int32_t blocks_per_cu, int32_t n_cu
  * crossover); CLV_PERSISTENT=1 forces it wherever it fits, =0 never. */
 int clv_debug_persist_choice(int32_t D, int32_t K, int32_t n_chains, int64_t grid_wgs, int32_t blocks_per_cu,
                              int32_t n_cu);
-/* Host only: the persistent grid's MH-variate producer / consumer roles for n_chains chains of nb
- * customer workgroups on n_cu CUs with up to n_off chunks per consumer and at most load_x100 / 100
- * tasks per producer on average (0: no cap) — out[linear workgroup][8]: [0] chunks taken from
- * producers, [1] tasks drawn for others, [2..] tasks (consumer << 4 | chunk); all zero when the
- * placement has no shared CUs to balance. */
-int clv_debug_pc_plan(int32_t n_chains, int32_t nb, int32_t n_cu, int32_t n_off, int32_t load_x100, int32_t* out);
 
 /* ---- In-process multi-device runs (SURVEY.md §8b devices=, §8e) ----
  * A group drives the n shards of one problem from one host thread: shards[r] = the sampler of rank

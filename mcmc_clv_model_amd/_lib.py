@@ -125,7 +125,6 @@ def lib() -> ctypes.CDLL:
         "clv_debug_wg_map": (c_int32, [c_int32, c_int32, c_int32, POINTER(c_int32)]),
         "clv_debug_persist_choice": (c_int32, [c_int32, c_int32, c_int32, c_int64, c_int32, c_int32]),
         "clv_debug_persist_fits": (c_int32, [c_int64, c_int32, c_int32]),
-        "clv_debug_pc_plan": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_int32, POINTER(c_int32)]),
         "clv_group_create": (c_int32, [POINTER(sp), c_int32, c_int32, POINTER(sp)]),
         "clv_group_run": (c_int32, [sp, c_int64]),
         "clv_group_exchange": (c_int32, [sp]),

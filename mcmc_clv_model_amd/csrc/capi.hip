@@ -72,8 +72,6 @@ SweepArgs sweep_args(clv_sampler* s, int init, int fuse = 0) {
   a.mail = s->d_mail;
   a.peers = s->d_peers;
   a.wg_map = s->d_wgmap;
-  a.pc_desc = s->d_pcdesc;
-  a.vbuf = s->d_vbuf;
   a.rank = s->cfg.rank;
   a.lam_out = s->d_lam_alt ? s->d_lam_alt : s->d_lam;
   a.mu_out = s->d_mu_alt ? s->d_mu_alt : s->d_mu;
@@ -256,16 +254,22 @@ bool clv::persist_grid_fits(int64_t grid_wgs, int blocks_per_cu, int n_cu) {
 // sweep, but all its customer waves stay resident, so once most CUs hold two workgroups the
 // doubled SIMDs (two waves each, issue-bound) set every sweep's period, where the launch-per-sweep
 // kernel runs 4 waves per SIMD and load-balances.  Measured crossover (tools/persist_crossover.py,
-// profiles/r04_persist_crossover*.jsonl; us per sweep persistent / launch-per-sweep): bivariate
-// K=2, 4 chains: 1.25 workgroups per CU 10.9 / 17.6, 1.61 12.6 / 18.7, 1.86 19.6 / 19.5; K=5,
-// 1 chain: 0.92 12.5 / 17.3, 1.38 21.0 / 20.8, 1.68 31.9 / 21.8, 1.91 43.8 / 22.4 (c4 at 8 ranks);
-// trivariate K=3, 4 chains: 1.25 12.5 / 20.3, 1.61 12.8 / 21.5.
+// profiles/r04_persist_crossover*.jsonl; us per sweep persistent / launch-per-sweep, workgroups
+// per CU):
+//   bivariate, 4 chains  K=2: 1.25 10.9 / 17.6, 1.61 12.6 / 18.7, 1.73 16.8 / 18.8, 1.86 19.6 / 19.5
+//                        K=5: 1.25 12.0 / 19.4, 1.61 13.9 / 20.4
+//   bivariate, 1-2 chains K=2: 0.92 8.0 / 15.7, 1.38 11.8 / 18.4, 1.68 22.8 / 19.5, 2 chains 1.84
+//                        23.6 / 19.2; K=5: 0.92 12.5 / 17.3, 1.38 21.0 / 20.8, 1.68 31.9 / 21.8,
+//                        1.91 43.8 / 22.4 (c4 at 8 ranks); K=9: 0.92 18.4 / 22.3, 1.38 29.9 / 29.8
+//   trivariate, 4 chains K=3: 1.25 12.5 / 20.3, 1.61 12.8 / 21.5; 1 chain K=3: 1.38 22.7 / 21.8,
+//                        1.68 26.7 / 23.1; K=9 (its persistent instance spills): 0.92 30.9 / 20.9
+// So: up to 1.75 workgroups per CU with 4+ chains, 1.45 (bivariate) / 1.25 (trivariate) with fewer,
+// never for the spilling trivariate instances (K >= 6).
 bool clv::persist_worth(int D, int K, int n_chains, int64_t grid_wgs, int n_cu) {
-  (void)D;
-  (void)K;
-  if (n_cu <= 0) return false;
+  if (n_cu <= 0 || (D == 3 && K >= 6)) return false;
   const double per_cu = (double)grid_wgs / n_cu;
-  return per_cu <= (n_chains >= 2 ? 1.65 : 1.35);
+  const double cap = n_chains >= 4 ? 1.75 : (D == 2 ? 1.45 : 1.25);
+  return per_cu <= cap;
 }
 
 namespace {
@@ -335,53 +339,6 @@ std::vector<int32_t> persist_wg_map(int C, int nb, int n_cu) {
   return map;
 }
 
-// MH-variate producers / consumers over the placement map above (kernels.hip pc_produce /
-// pc_consume): the customer workgroups of shared CUs (linear [C, P) and n_cu + [C, P), where
-// P = T - n_cu) are consumers that leave their first n_i chunks of drawn-ahead MH variates to
-// customer workgroups OF THE SAME CHAIN alone on their CUs (linear [P, n_cu) and the level-2
-// workgroups' partners n_cu + [0, C)), which draw them right after their own block partial.  Per
-// chain, chunk q goes to the chain's consumers in order (round robin over its producers, at most
-// PC_DESC - 2 tasks each, at most load_x100 / 100 on average when load_x100 > 0), so n_i is the
-// same for all of a chain's consumers or one less.  Same-chain dealing matters: a consumer waits
-// for its producers' sweep, so a producer of another chain couples the chains' paces.  Measured at
-// c2.  Empty if the map is not the paired placement.
-std::vector<int32_t> pc_plan(const std::vector<int32_t>& map, int C, int nb, int n_cu, int n_off, int load_x100) {
-  const int T = (int)map.size();
-  const int P = T - n_cu;
-  std::vector<int32_t> desc;
-  if (n_off <= 0 || P <= C || T > 2 * n_cu || T != C * (nb + 1)) return desc;
-  for (int c = 0; c < C; ++c)  // the paired placement: level-2 workgroups first (persist_wg_map)
-    if (map[c] != ((c << 16) | nb)) return desc;
-  std::vector<std::vector<int>> cons(C), prod(C);
-  for (int i = C; i < P; ++i) cons[map[i] >> 16].push_back(i);
-  for (int i = n_cu + C; i < n_cu + P; ++i) cons[map[i] >> 16].push_back(i);
-  for (int i = P; i < n_cu; ++i) prod[map[i] >> 16].push_back(i);
-  for (int i = n_cu; i < n_cu + C; ++i) prod[map[i] >> 16].push_back(i);
-  for (int c = 0; c < C; ++c)
-    for (int i : prod[c])
-      if ((map[i] & 0xFFFF) == nb) return desc;  // (a level-2 workgroup is never a producer)
-  const int per = PC_DESC - 2;
-  desc.assign((size_t)T * PC_DESC, 0);
-  bool any = false;
-  for (int c = 0; c < C; ++c) {
-    const std::vector<int>& cs = cons[c];
-    const std::vector<int>& ps = prod[c];
-    if (cs.empty() || ps.empty()) continue;
-    int64_t budget = std::min((int64_t)cs.size() * n_off, (int64_t)ps.size() * per);
-    if (load_x100 > 0) budget = std::min(budget, (int64_t)ps.size() * load_x100 / 100);
-    int64_t t = 0;
-    for (int q = 0; q < n_off && t < budget; ++q)  // chunk by chunk: prefixes [0, n_i) per consumer
-      for (size_t k = 0; k < cs.size() && t < budget; ++k, ++t) {
-        const int i = cs[k];
-        desc[(size_t)i * PC_DESC] = q + 1;
-        int32_t* d = &desc[(size_t)ps[t % ps.size()] * PC_DESC];
-        d[2 + d[1]++] = (i << 4) | q;
-        any = true;
-      }
-  }
-  if (!any) desc.clear();
-  return desc;
-}
 }  // namespace
 
 extern "C" {
@@ -587,23 +544,6 @@ int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* pri
       std::vector<int32_t> map = persist_wg_map((int)C, (int)nb_local, s->n_cu);
       CLV_HIPC(dalloc(&s->d_wgmap, map.size()));
       CLV_HIPC(hipMemcpy(s->d_wgmap, map.data(), sizeof(int32_t) * map.size(), hipMemcpyHostToDevice));
-      // world size 1: producer / consumer split of the drawn-ahead MH variates (CLV_PC_CHUNKS:
-      // chunks per consumer, default 1, 0 = off; c2 at 5,000 sweeps: 0 10.87, 1 10.74, 2 14.0, 3
-      // 15.8 us per sweep); full 4-step chunks of drawn-ahead variates only
-      env = std::getenv("CLV_PC_CHUNKS");
-      const int n_off = std::min({env ? std::atoi(env) : 1, g.S / MH_CHUNK_STEPS, PC_CHUNKS});
-      const int load_x100 = 0;  // (no cap on a producer's tasks: capping measured slower)
-      if (s->persistent && s->pre_variates && g.S <= PC_CHUNKS * MH_CHUNK_STEPS && n_off > 0) {
-        const std::vector<int32_t> desc = pc_plan(map, (int)C, (int)nb_local, s->n_cu, n_off, load_x100);
-        if (!desc.empty()) {
-          CLV_HIPC(dalloc(&s->d_pcdesc, desc.size()));
-          CLV_HIPC(hipMemcpy(s->d_pcdesc, desc.data(), sizeof(int32_t) * desc.size(), hipMemcpyHostToDevice));
-          s->n_vbuf = 2LL * (int64_t)map.size() * PC_CHUNKS * PC_WORDS * BLOCK;
-          CLV_HIPC(dalloc(&s->d_vbuf, (size_t)s->n_vbuf));
-          CLV_HIPC(hipMemset(s->d_vbuf, 0xFF, sizeof(double) * (size_t)s->n_vbuf));  // every slot empty
-          s->pc_chunks = desc[(size_t)C * PC_DESC];
-        }
-      }
     }
   }
 #ifdef CLV_STAMPS
@@ -719,8 +659,6 @@ void clv_destroy(clv_sampler* s) {
   if (s->d_mail) (void)hipFree(s->d_mail);
   if (s->d_peers) (void)hipFree(s->d_peers);
   if (s->d_wgmap) (void)hipFree(s->d_wgmap);
-  if (s->d_pcdesc) (void)hipFree(s->d_pcdesc);
-  if (s->d_vbuf) (void)hipFree(s->d_vbuf);
   if (s->own_stream && s->own) (void)hipStreamDestroy(s->own);
   delete s;
 }
@@ -817,7 +755,7 @@ int clv_launch_info(const clv_sampler* s, int64_t* out) {
   out[1] = s->persist_bpc;
   out[2] = s->n_cu;
   out[3] = (int64_t)(s->g.nb_local + (s->persistent ? 1 : 0)) * s->g.n_chains;
-  out[4] = s->pc_chunks;
+  out[4] = 0;  // (reserved: was the MH-variate producer / consumer chunks, removed in round 4)
   out[5] = 0;  // (reserved: was the stride kernel's grid, removed)
   return CLV_OK;
 }
@@ -938,7 +876,6 @@ int clv::persist_launch(clv_sampler* s, int64_t n_sweeps) {
     // every hand-off slot empty (all-ones bytes: the sentinel NaN)
     CLV_HIP(hipMemsetAsync(s->d_hyp2, 0xFF, sizeof(double) * 2 * g.n_chains * HS, s->stream));
     CLV_HIP(hipMemsetAsync(s->d_pblock, 0xFF, sizeof(double) * g.n_chains * g.nb_local * g.stride, s->stream));
-    if (s->d_vbuf) CLV_HIP(hipMemsetAsync(s->d_vbuf, 0xFF, sizeof(double) * (size_t)s->n_vbuf, s->stream));
     s->slots_dirty = false;
   }
   const size_t sums_bytes = sizeof(double) * (size_t)g.n_chains * CLV_N_SUM_STATS * g.n;
@@ -1462,16 +1399,6 @@ int clv_debug_hyper_variates(uint64_t seed, int32_t chain, uint32_t sweep, doubl
   CLV_HIP(hipMemcpy(normals, dn, sizeof(double) * n, hipMemcpyDeviceToHost));
   CLV_HIP(hipFree(dc));
   CLV_HIP(hipFree(dn));
-  return CLV_OK;
-}
-
-int clv_debug_pc_plan(int32_t n_chains, int32_t nb, int32_t n_cu, int32_t n_off, int32_t load_x100, int32_t* out) {
-  if (!out || n_chains < 1 || nb < 0 || n_cu < 1 || n_chains >= (1 << 15) || nb >= (1 << 16))
-    return fail(CLV_EINVAL, "bad arguments");
-  const std::vector<int32_t> d = pc_plan(persist_wg_map(n_chains, nb, n_cu), n_chains, nb, n_cu, n_off, load_x100);
-  const size_t T = (size_t)n_chains * (nb + 1);
-  if (d.empty()) std::fill(out, out + T * PC_DESC, 0);
-  else std::copy(d.begin(), d.end(), out);
   return CLV_OK;
 }
 

@@ -119,10 +119,6 @@ struct clv_sampler {
   int mail_kind = -1;               // the mail's memory: 0 uncached, 1 fine-grained, 2 plain device memory
   double** d_peers = nullptr;       // [world] mail pointers (peers' opened IPC mappings, own d_mail)
   int32_t* d_wgmap = nullptr;       // persistent grid: linear workgroup -> (chain << 16 | block)
-  int32_t* d_pcdesc = nullptr;      // persistent grid: MH-variate producer / consumer roles (pc_plan)
-  double* d_vbuf = nullptr;         // their hand-off slots
-  int64_t n_vbuf = 0;
-  int pc_chunks = 0;                // chunks per consumer (0: no producer / consumer split)
   std::vector<void*> ipc_opened;    // hipIpcOpenMemHandle mappings to close
   double* d_hvar = nullptr;         // [chain][HV] precomputed hyper variates
   unsigned long long* d_stamps = nullptr;  // CLV_STAMPS diagnostic build only

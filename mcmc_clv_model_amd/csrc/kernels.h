@@ -14,9 +14,6 @@ constexpr int TAPE_HYPER = 40;         // doubles of hyper variates per recorded
 constexpr int MAX_WORLD = 64;             // peer exchange: ranks (mail pointers staged in LDS)
 constexpr int UMAIL = 2048;            // persistent kernel, world size > 1: LDS doubles for this rank's
                                        // unit partials (stride * local units must fit)
-constexpr int PC_DESC = 8;              // producer/consumer role record per workgroup (int32)
-constexpr int PC_WORDS = 6;             // 8-byte words per lane and 4-step chunk: (t_l, t_m) x 4, (log2 u) x 4
-constexpr int PC_CHUNKS = 5;            // chunks of the drawn-ahead MH variates (PRE_STEPS / 4)
 constexpr int HV = 40;                 // precomputed Philox hyper variates per chain: iw normals [0,3),
                                        // chi2 [3,6), beta normals [8,35)
 
@@ -115,13 +112,6 @@ struct SweepArgs {
   int rank;
   const int32_t* wg_map;     // persistent kernel: linear workgroup -> (chain << 16 | block), or null
   int pre_variates;          // persistent kernel: draw the next sweep's MH variates during the hand-off
-  // persistent kernel, world size 1: MH-variate producers / consumers (SIMD balancing, capi.hip
-  // pc_plan).  pc_desc[linear workgroup][PC_DESC]: [0] chunks of its own next-sweep MH variates
-  // this workgroup reads from vbuf instead of drawing them (consumer), [1] number of chunk tasks
-  // it draws for consumers (producer), [2..] tasks (consumer linear workgroup << 4 | chunk).
-  // vbuf: [2 (sweep parity)][linear workgroup][PRE_CHUNKS][PC_WORDS][BLOCK] packed float pairs.
-  const int32_t* pc_desc;
-  double* vbuf;
   // persistent kernel: the carried state at the end of a launch goes to these (the host swaps them
   // with lam / mu / hyper only if no wave aborted), the bound on every wait (s_memrealtime ticks,
   // 100 MHz) and a host-mapped copy of ctrl->abort (read by the host after the launch, no D2H copy)

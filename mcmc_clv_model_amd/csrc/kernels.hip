@@ -1295,14 +1295,13 @@ __device__ __forceinline__ int opaque_uniform(int x) {
   return x;
 }
 
-// q_first: chunks below it come from producer workgroups (pc_consume) and are not drawn here.
 template <int NQ = PRE_STEPS / MH_CHUNK_STEPS>
-__device__ __forceinline__ void mh_pre_variates(const SlotPhilox& ph, int S_, const PreVariates& v, int q_first = 0) {
+__device__ __forceinline__ void mh_pre_variates(const SlotPhilox& ph, int S_, const PreVariates& v) {
   constexpr int MC = MH_CHUNK_STEPS;
   const int S = opaque_uniform(S_);
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
-    if (q >= q_first && q * MC < S) {  // wave-uniform
+    if (q * MC < S) {  // wave-uniform
       float tl[MC], tm[MC], lu[MC];
       mh_chunk_variates(ph, (uint32_t)q, tl, tm, lu);
       if (q * MC + MC <= S) {  // full chunk
@@ -1507,9 +1506,6 @@ static_assert(BLOCK == EXP_TAB_N, "the sweep kernel stages the exp table with on
 // FX: the fused peer exchange (world size > 1 after clv_p2p_connect) compiled in — instances of
 // their own, launched for sharded runs only (compiled into the world-size-1 kernels it cost c4 /
 // c5 1.8% / 1.6% per sweep).
-#ifndef CLV_TAIL_STORE_LATE
-#define CLV_TAIL_STORE_LATE 1
-#endif
 template <int D, int K, bool REPLAY, bool FX>
 __device__ __forceinline__ void sweep_body(const SweepArgs& a) {
   constexpr int NT = BLOCK;
@@ -1766,12 +1762,9 @@ __device__ __forceinline__ void sweep_body(const SweepArgs& a) {
     }
     __syncthreads();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only
-    // the chain's last unit stores after its level-2 draw: the draw's loads would otherwise wait
-    // (vmcnt counts in order) for the sums' and draws' stores, on every sweep's serial tail
-    // (bivariate instances: the trivariate ones would hold the stores' operands across the draw at
-    // 149 instead of 125 VGPRs, 3 instead of 4 waves per SIMD)
-    constexpr bool LATE = CLV_TAIL_STORE_LATE && D == 2;
-    if (!LATE || !s_last) finish_store();
+    // (storing after the chain's last unit's level-2 draw instead, so that the draw's loads do not
+    // wait for these stores in vmcnt order, measured 0.5-1.2 us per sweep slower at c4, round 4)
+    finish_store();
     if (s_last) {
       if (threadIdx.x == 0) CLV_STAMP(a.stamps, s, 2, false);
       if (!fx) {
@@ -1835,7 +1828,6 @@ __device__ __forceinline__ void sweep_body(const SweepArgs& a) {
         }
       }
       if (threadIdx.x == 0) CLV_STAMP(a.stamps, s, 3, false);
-      if (LATE) finish_store();
     }
   }
 }
@@ -1847,11 +1839,8 @@ template <int D, int K, bool REPLAY, bool FX>
 __global__ __launch_bounds__(BLOCK) void sweep_kernel(SweepArgs a) {
   sweep_body<D, K, REPLAY, FX>(a);
 }
-#ifndef SWEEP_OCC_WAVES  // (A/B builds: the occupancy target of the occ4 instances)
-#define SWEEP_OCC_WAVES 4
-#endif
 template <int D, int K, bool REPLAY, bool FX>
-__global__ __launch_bounds__(BLOCK, SWEEP_OCC_WAVES) void sweep_kernel_occ4(SweepArgs a) {
+__global__ __launch_bounds__(BLOCK, 4) void sweep_kernel_occ4(SweepArgs a) {
   sweep_body<D, K, REPLAY, FX>(a);
 }
 
@@ -2196,79 +2185,6 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
   return;
 }
 
-#ifndef CLV_PC_BUILD  // (A/B: 0 compiles the producer / consumer hand-off out of the persistent kernel)
-#define CLV_PC_BUILD 1
-#endif
-// ---- MH-variate producers and consumers (persistent kernel, world size 1; capi.hip pc_plan) ----
-// c2 runs 1,473 customer wavefronts on 1,024 SIMDs: the SIMDs of the CUs that hold two workgroups
-// run two wavefronts and set the sweep period, the others idle part of it.  The drawn-ahead MH
-// variates of the next sweep are independent of the state, so consumer workgroups (on shared CUs)
-// leave their first chunks to producer workgroups (alone on their CUs), which draw them for the
-// consumer's customers (same Philox counters: same values, same results bit for bit) in their
-// hand-off window and store them as packed float pairs into vbuf; the consumer reads them at the
-// start of that sweep.  A word is its own arrival flag (the all-ones pattern is never a pair of
-// finite floats): the consumer polls until its words are there, copies them to its LDS pool and
-// empties the slots.  Slot reuse (sweep s + 2) follows the level-2 hand-off: a producer writes
-// them only after (beta, Sigma) of s + 1, published after the consumer's partial of s, which
-// leaves after its resets (write-through stores, each wave waiting for its own right after
-// pc_consume, before the (beta, Sigma) wait).
-__device__ __forceinline__ double pack_f2(float lo, float hi) {
-  return bitsd((uint64_t)__float_as_uint(lo) | ((uint64_t)__float_as_uint(hi) << 32));
-}
-__device__ __forceinline__ float lo_f(double w) { return __uint_as_float((uint32_t)dbits(w)); }
-__device__ __forceinline__ float hi_f(double w) { return __uint_as_float((uint32_t)(dbits(w) >> 32)); }
-
-__device__ __forceinline__ double* pc_slot(const SweepArgs& a, int64_t s, int T, int L, int q) {
-  return a.vbuf + (((int64_t)(s & 1) * T + L) * PC_CHUNKS + q) * PC_WORDS * BLOCK;
-}
-
-// Producer: chunk q of the MH variates of sweep s for consumer workgroup `cons`'s customers.
-__device__ __forceinline__ void pc_produce(const SweepArgs& a, int32_t task, int64_t s, int T, int tid) {
-  const int cons = task >> 4, q = task & 15;
-  const int32_t m = a.wg_map[cons];
-  uint32_t kk0, kk1;
-  chain_key(a.r.seed, (int64_t)a.r.chain_first + (m >> 16), &kk0, &kk1);
-  const uint32_t gi = (uint32_t)(a.g.shard_begin + (int64_t)(m & 0xFFFF) * BLOCK + tid);
-  float tl[MH_CHUNK_STEPS], tm[MH_CHUNK_STEPS], lu[MH_CHUNK_STEPS];
-  mh_chunk_variates(SlotPhilox(kk0, kk1, gi, (uint32_t)s), (uint32_t)q, tl, tm, lu);
-  double* dst = pc_slot(a, s, T, cons, q) + tid;
-#pragma unroll
-  for (int w = 0; w < MH_CHUNK_STEPS; ++w) st_wt(dst + w * BLOCK, pack_f2(tl[w], tm[w]));
-  st_wt(dst + 4 * BLOCK, pack_f2(lu[0], lu[1]));
-  st_wt(dst + 5 * BLOCK, pack_f2(lu[2], lu[3]));
-}
-
-// Consumer: chunks [0, n_off) of this workgroup's MH variates of sweep s into the LDS pool, slots
-// emptied after.  False if a wait timed out (the abort flag is raised: every wave leaves at its
-// next wait).
-__device__ __forceinline__ bool pc_consume(const SweepArgs& a, int n_off, int64_t s, int T, int L, const PreVariates& v) {
-  for (int q = 0; q < n_off; ++q) {
-    double* src = pc_slot(a, s, T, L, q) + v.lane;
-    double w[PC_WORDS];
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    for (uint32_t poll = 0;; ++poll) {
-      bool ok = true;
-#pragma unroll
-      for (int k = 0; k < PC_WORDS; ++k) {
-        w[k] = ld_wt(src + k * BLOCK);
-        ok = ok & slot_full(w[k]);
-      }
-      if (__all(ok)) break;
-      if (wait_expired(a, t0, poll)) return false;
-      __builtin_amdgcn_s_sleep(1);
-    }
-#pragma unroll
-    for (int k = 0; k < MH_CHUNK_STEPS; ++k) v.t[(q * MH_CHUNK_STEPS + k) * BLOCK + v.lane] = make_float2(lo_f(w[k]), hi_f(w[k]));
-    v.u[(q * MH_CHUNK_STEPS + 0) * BLOCK + v.lane] = lo_f(w[4]);
-    v.u[(q * MH_CHUNK_STEPS + 1) * BLOCK + v.lane] = hi_f(w[4]);
-    v.u[(q * MH_CHUNK_STEPS + 2) * BLOCK + v.lane] = lo_f(w[5]);
-    v.u[(q * MH_CHUNK_STEPS + 3) * BLOCK + v.lane] = hi_f(w[5]);
-#pragma unroll
-    for (int k = 0; k < PC_WORDS; ++k) st_wt(src + k * BLOCK, slot_empty());
-  }
-  return true;
-}
-
 // The kernel arguments re-read from the kernarg segment through an opaque pointer: in a loop over
 // tasks the compiler otherwise loads every argument once at entry and keeps them all live in SGPRs
 // (hundreds of SGPR spills into VGPR lanes), instead of scalar loads where they are used.
@@ -2313,13 +2229,6 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
   const int tid = threadIdx.x;
   const int64_t wgi = (int64_t)c * (g.nb_local + 1) + b;
   const int64_t it_stamp = n_sweeps >= 2 ? n_sweeps - 2 : 0;  // diagnostic build: one sweep's timeline
-  // producer / consumer role of this (dispatch-order) workgroup; none in the P2P instance
-  const int T_wg = gridDim.x * gridDim.y, L_wg = blockIdx.y * gridDim.x + blockIdx.x;
-  int pc_off = 0, pc_ntask = 0;
-  if (!P2P && CLV_PC_BUILD && a.pc_desc) {
-    pc_off = a.pc_desc[L_wg * PC_DESC];
-    pc_ntask = a.pc_desc[L_wg * PC_DESC + 1];
-  }
   (void)wgi;
   (void)it_stamp;
   uint32_t k0, k1;
@@ -2369,14 +2278,6 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
     const bool stp = tid == 0 && it == it_stamp;
     (void)stp;
     CLV_P_STAMP(a.stamps, wgi, 0, stp);
-    // consumer: this sweep's first MH-variate chunks from the producers (drawn during sweep s - 1)
-    if (pc_off > 0 && it > 0 && pre) {
-      if (!pc_consume(a, pc_off, s, T_wg, L_wg, pv)) s_abort = 1;
-      // the slot resets (every wave's own write-through stores) complete before this sweep's partial
-      // can leave, so a producer's store for sweep s + 2 never meets a reset still in flight (ADVICE
-      // r3: the ordering the slot reuse relies on, made explicit; it overlaps the (beta, Sigma) wait)
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
     if (it > 0 || (!P2P && a.pend_in)) {  // wait for (beta, Sigma) of sweep s (wavefront 0 polls, one slot per lane)
       if (tid < 64) {
         const double* src = hyp_c + (int64_t)(s & 1) * g.n_chains * HS;
@@ -2432,16 +2333,11 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
 #ifdef CLV_STAMPS
     if (stp && a.stamps) a.stamps[1024 * 8 + wgi * 12 + 11] = blockIdx.y * gridDim.x + blockIdx.x;  // dispatch position
 #endif
-    // producer: consumers' chunks of sweep s + 1 (every lane: the consumer polls all of its lanes),
-    // before this workgroup's own next-sweep work — the consumers need them as soon as (beta, Sigma)
-    // of s + 1 arrive (drawn after the own work: c2 10.83 instead of 10.73 us per sweep)
-    if (pre && it + 1 < n_sweeps)
-      for (int k = 0; k < pc_ntask; ++k) pc_produce(a, a.pc_desc[L_wg * PC_DESC + 2 + k], s + 1, T_wg, tid);
     if (cu.active) {
       cust_store<D, K>(cu, out, a, c, s, stored, false);
       if (it + 1 < n_sweeps) {
         cust_ztau<D, K, false>(cu, a, s + 1, k0, k1, nullptr, exp_tab);
-        if (pre) mh_pre_variates(SlotPhilox(k0, k1, cu.gi, (uint32_t)(s + 1)), g.S, pv, pc_off);
+        if (pre) mh_pre_variates(SlotPhilox(k0, k1, cu.gi, (uint32_t)(s + 1)), g.S, pv);
         if constexpr (D == 3) {
           if (pre) zeta_lds[tid] = eta_normal(k0, k1, cu.gi, s + 1, exp_tab);
         }

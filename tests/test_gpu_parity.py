@@ -555,13 +555,9 @@ def test_persistent_kernel_bitwise_equals_launch_per_sweep(L, monkeypatch, D, co
     p = build_problem(df, covs, D)
     kw = dict(mcmc=25, burnin=6, thin=3, chains=3, seed=2024, draw_sink=sink, n_mh_steps=S)
     chunks = (1, 7, 2, 20, 1)
-    if D == 2 and n == 23570:  # (the producer / consumer split at 3 chunks, beyond its default 1)
-        monkeypatch.setenv("CLV_PC_CHUNKS", "3")
     a = _run_mode(p, True, 31, chunks, **kw)
     b = _run_mode(p, False, 31, chunks, **kw)
     assert a[0]["persistent"] and not b[0]["persistent"], (a[0], b[0])
-    if D == 2 and n == 23570:  # 3 chains x 94 workgroups on 256 CUs: MH-variate producers / consumers
-        assert a[0]["pc_chunks"] == 3, a[0]
     for x, y in zip(a[1], b[1]):
         assert np.array_equal(bits(x), bits(y))
     for x, y in zip(a[2:], b[2:]):
@@ -632,27 +628,6 @@ def test_deferred_level2_draw_bitwise(L, D, covs, sink):
     a = _run_ops(p, {"CLV_PERSISTENT": "1", "CLV_DEFER": "1"}, rb, **kw)
     b = _run_ops(p, {"CLV_PERSISTENT": "1", "CLV_DEFER": "1"}, straight, **kw)
     _same_bits(a[1:], b[1:])
-
-
-@pytest.mark.parametrize("chunks", ["0", "1", "2"])
-def test_producer_consumer_variates_bitwise(L, monkeypatch, chunks):
-    """c2's layout (4 chains x 23,570 customers: 376 workgroups on 256 CUs): consumer workgroups on
-    shared CUs read their first MH-variate chunks from producer workgroups (CLV_PC_CHUNKS chunks,
-    default 1) — bitwise the same run as without the split (CLV_PC_CHUNKS=0)."""
-    from mcmc_clv_model_amd.sampler import build_problem
-    p = build_problem(cdnow("full"), ["first_sales_scaled"], 2)
-    kw = dict(mcmc=12, burnin=8, thin=2, chains=4, seed=31, draw_sink="summary", n_mh_steps=20)
-    monkeypatch.setenv("CLV_PC_CHUNKS", "3")
-    ref = _run_mode(p, True, 20, (3, 17), **kw)
-    assert ref[0]["pc_chunks"] == 3, ref[0]
-    monkeypatch.setenv("CLV_PC_CHUNKS", chunks)
-    got = _run_mode(p, True, 20, (3, 17), **kw)
-    assert got[0]["pc_chunks"] == int(chunks), got[0]
-    for x, y in zip(ref[1], got[1]):  # state
-        assert np.array_equal(bits(x), bits(y))
-    for x, y in zip(ref[2:], got[2:]):  # draws, level 2, log-likelihood, summaries
-        if x is not None:
-            assert np.array_equal(bits(x), bits(y))
 
 
 def _mh_step_device(L, f, t3, log_u, cur_pt=None):

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (Measured in round 4 before the producer / consumer hand-off was removed: its CLV_PC_CHUNKS arms and build/nopc refer to that code.)
 # Round 4, third batch: persistent / launch crossover (second case set); c2 with the producer /
 # consumer hand-off (chunks 1), without it (chunks 0) and compiled out (build/nopc), two passes;
 # the driver step with the timed launch bracketed by hipEventRecord vs the dispatch's timestamps.
