@@ -260,6 +260,13 @@ def measure_config(name: str, world: int, rank: int, local_rank: int, dist, step
     # read-modify-writes the customer's running sums, bi:402-428): continue the same chains into
     # it, 100 sweeps past the boundary (warm), then time `steps` stored sweeps
     phases = None
+    K = len(covs) + 1
+    kname = "sweep_kernel"  # (c4 / c5: launch-per-sweep; the committed profiles are of that kernel)
+
+    def traffic(tag):  # calibrated PMC bytes per (chain, customer) sweep from the committed profile
+        tr = committed_traffic(tag, False, kname, D, K) if world == 1 else None
+        return None if not tr else dict(bytes_per_unit=round(tr["bytes_per_sweep"] / (chains * n_total), 2),
+                                        source=tr["source"])
     if stored_phase and burnin > warmup + steps:
         done = warmup + steps
         run(burnin + 100 - done)
@@ -273,7 +280,8 @@ def measure_config(name: str, world: int, rank: int, local_rank: int, dist, step
         phases = dict(
             stored=dict(value=v_st, ms_per_step=t_s * 1e3, sweeps=f"{first}..{first + steps - 1}",
                         bytes_per_unit=round(bpu_st, 2),
-                        hbm_frac=round(bpu_st * v_st / 1e9 / (world * HBM_PEAK_GBS), 5)),
+                        hbm_frac=round(bpu_st * v_st / 1e9 / (world * HBM_PEAK_GBS), 5),
+                        measured_traffic=traffic(f"{name}stored")),
             whole_run=dict(value=whole, sweeps=f"{burnin} burn-in + {mcmc0} stored",
                            note="customer-sweeps/s of the BASELINE run from the two phases' per-sweep times"))
     linfo = kern.launch_info()
@@ -281,7 +289,6 @@ def measure_config(name: str, world: int, rank: int, local_rank: int, dist, step
     exch = getattr(kern, "exchange", None)
     note = getattr(kern, "p2p_note", None)
     kern.close()
-    K = len(covs) + 1
     value = chains * n_total * steps / dt
     bpu = algorithmic_bytes(D, K, stored_fraction(burnin, thin, warmup + 1, warmup + steps), sink)
     data = WORKLOADS[name][1]
@@ -297,7 +304,8 @@ def measure_config(name: str, world: int, rank: int, local_rank: int, dist, step
                       (", unit partials stored into every rank's mail over xGMI by the kernel (no host collective)"
                        if exch == "p2p" else ", RCCL all-gather + level-2 kernel per sweep") +
                       (f" ({note})" if note else "")),
-                phase=f"burn-in (sweeps {warmup + 1}..{warmup + steps})", **(phases or {}))
+                phase=f"burn-in (sweeps {warmup + 1}..{warmup + steps})", measured_traffic=traffic(name),
+                **(phases or {}))
 
 
 def main():
@@ -415,6 +423,7 @@ def main():
     if dist:
         dist.barrier()
     dt = time.perf_counter() - t0
+    host_us = kern.host_times() if (persistent and not sharded) else None  # where the step's host time went
     kt_live = None
     if live:
         kt_live = kern.kernel_time()
@@ -534,6 +543,8 @@ def main():
                         f"torch.cuda graph replay ({a.graph_chunk} sweeps: sweep + group kernels, RCCL all_gather, "
                         "level-2 kernel)" if a.graph_chunk else "eager: sweep + group kernels, RCCL all_gather, level-2"),
             roofline=roofline, cpu_baseline=cpu,
+            host_us=(dict(host_us, clv_run_total=round(sum(host_us.values()), 3), timed_region=round(dt * 1e6, 3))
+                     if host_us else None),
             exchange=(None if world == 1 and not sharded else
                       dict(kind=kern.exchange, note=kern.p2p_note, requested=a.exchange if world > 1 else "rccl")),
             speedup_vs_cpu_1core=(value / cpu["value"]) if cpu else None,

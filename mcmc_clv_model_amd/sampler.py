@@ -237,6 +237,18 @@ class HipSampler:
     def synchronize(self) -> None:
         check(self._L.clv_synchronize(self.h))
 
+    def host_times(self) -> dict:
+        """clv_debug_host_times of the last persistent clv_run, as microsecond splits: hipSetDevice,
+        the start event's record, the launch call, the end event's record, the wait for the end,
+        the return path."""
+        hn = (ctypes.c_int64 * 8)()
+        check(self._L.clv_debug_host_times(self.h, hn))
+        h = [x / 1e3 for x in hn]
+        if not h[0] or not h[6]:
+            return {}
+        names = ("set_device", "start_event", "launch_call", "end_event", "wait", "return")
+        return {k: round(h[i + 1] - h[i], 3) for i, k in enumerate(names)}
+
     def launch_info(self) -> dict:
         """How clv_run launches (clv_launch_info): persistent kernel or one launch per sweep."""
         out = (ctypes.c_int64 * 6)()
