@@ -1674,12 +1674,18 @@ __device__ __forceinline__ void sweep_body(const SweepArgs& a) {
   // issued after the hand-off's ticket and never waited for (the tail never reads them).  Was: the
   // whole cust_store between the partial and the drain — two round trips per workgroup, +8.5% per
   // stored sweep at c4 / c5.
+  // The sharded fused-exchange instances (FX, world size > 1) keep round 3's placement — the whole
+  // cust_store before the hand-off's drain: with the stores after the ticket, the two-process
+  // rehearsal of c4 on one GPU (tools/gpu_rehearse_n2.sh) timed out in the peer exchange twice in
+  // two runs, with this placement it ran (0.112 ms per sweep) — kept until it is understood.
   const bool has_store = !a.init && cu.active;
+  constexpr bool EARLY = FX;
+  if (EARLY && has_store) cust_store<D, K>(cu, out, a, c, s, stored, true);
   SumsPre<D> pre;
-  const bool pre_sums = !REPLAY && has_store && stored && a.sums != nullptr;
+  const bool pre_sums = !EARLY && !REPLAY && has_store && stored && a.sums != nullptr;
   if (pre_sums) prefetch_sums<D>(a, c, cu.i, pre);
   auto finish_store = [&]() {
-    if (has_store) cust_store<D, K>(cu, out, a, c, s, stored, true, pre_sums ? &pre : nullptr);
+    if (!EARLY && has_store) cust_store<D, K>(cu, out, a, c, s, stored, true, pre_sums ? &pre : nullptr);
   };
   if (!a.fuse) finish_store();
 
