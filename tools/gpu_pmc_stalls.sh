@@ -3,7 +3,9 @@
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R; export TMPDIR=/tmp
 W=${1:-c2}
 mkdir -p gpurun_out/pmc_$W
-B="python3 $R/bench.py --workload $W --no-cpu-baseline --no-kernel-timing --steps 200 --warmup 50"
+K=${2:-persist_kernel}
+# two dispatches (50 warm-up + 200 sweeps) of the workload only: tools/pmc_run.py
+B="python3 $R/tools/pmc_run.py $W 50 200"
 i=0
 for P in "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_BUSY_CYCLES" \
          "SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_SALU SQ_INSTS_VMEM" \
@@ -12,5 +14,6 @@ for P in "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_AN
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc $P -d $R/gpurun_out/pmc_$W/p$i -o run --output-format csv -- $B > gpurun_out/pmc_${W}_p$i.log 2>&1; rc=$?; echo ${W}_p${i}_rc=$rc
   [ $rc -eq 0 ] || exit $rc
+  python3 $R/tools/pmc_reduce.py $R/gpurun_out/pmc_$W/p$i $K && rm -rf $R/gpurun_out/pmc_$W/p$i
 done
 exit 0
