@@ -205,8 +205,28 @@ def cpu_baseline(workload: str, warm: int = 20, timed: int = 200, parallel: bool
     return res
 
 
+def settle_clocks(ms: float, device: int) -> float:
+    """Hold the GPU busy for `ms` of wall time with fp64 matmuls (work unrelated to the sampler,
+    outside every timed region), so that a short timed window runs at the clocks a whole run sees:
+    the driver's 20-sweep window after 5 one-sweep warm-up calls otherwise starts from the idle
+    power state and pays ~0.85 us per sweep of clock ramp (tools/driver_breakdown.py, cases cold /
+    after_busy / after_long / long_then_idle: profiles/r04_clock_ramp.jsonl).  Returns the seconds
+    spent."""
+    import torch
+    if ms <= 0:
+        return 0.0
+    a = torch.randn(2048, 2048, dtype=torch.float64, device=f"cuda:{device}")
+    b = a
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < ms / 1e3:
+        b = torch.tanh(a @ b * 1e-3)
+        torch.cuda.synchronize()
+    del a, b
+    return time.perf_counter() - t0
+
+
 def measure_config(name: str, world: int, rank: int, local_rank: int, dist, steps: int, warmup: int,
-                   graph_chunk: int, exchange: str, stored_phase: bool = True) -> dict:
+                   graph_chunk: int, exchange: str, stored_phase: bool = True, settle_ms: float = 0.0) -> dict:
     """One BASELINE multi-GPU configuration at this world size: c4 = 1M bivariate
     customers K=5 sharded over the ranks (strong scaling: the same problem at every N), c5 = 1.25M
     trivariate customers K=9 per rank (weak scaling).  Wall time of `steps` sweeps (max over ranks)
@@ -253,6 +273,7 @@ def measure_config(name: str, world: int, rank: int, local_rank: int, dist, step
             dt = float(t.item())
         return dt
 
+    settle_clocks(settle_ms, local_rank)  # (the problem build above left the GPU idle for seconds)
     run(warmup)
     sync()
     dt = timed(steps)  # burn-in sweeps warmup+1 .. warmup+steps
@@ -339,6 +360,9 @@ def main():
     ap.add_argument("--one-gpu-rehearsal", action="store_true",
                     help="world size > 1 on a one-GPU box: every rank on device 0, gloo process group (the "
                          "exchange paths are exercised; the numbers are not a scaling measurement)")
+    ap.add_argument("--clock-settle-ms", type=float, default=100.0,
+                    help="GPU busy time (fp64 matmuls, unrelated work) just before the warm-up, so the timed "
+                         "window starts at the clocks of a running job, not the idle power state; 0 = off")
     ap.add_argument("--cpu-baseline-child", action="store_true")
     ap.add_argument("--cpu-warm", type=int, default=20)
     ap.add_argument("--cpu-timed", type=int, default=200)
@@ -410,6 +434,7 @@ def main():
     # through that same path (events included, their times discarded), so the timed call is not
     # the first of its kind in the process
     live = timing and one_launch
+    settle_s = settle_clocks(a.clock_settle_ms, local_rank)
     if live:
         kern.set_timing(True)
     if one_launch:  # the warm-up steps one call each: the host path of a call is warm when timed
@@ -514,13 +539,14 @@ def main():
         # warm-up of 200 sweeps (the launch-per-sweep path captures its 64-sweep hipGraph on first use;
         # clocks ramp), then 1,000 timed sweeps: c4 ~0.09 s, c5 ~0.13 s per GPU
         extra[name] = measure_config(name, world, rank, local_rank, dist, a.scaling_steps, 200, a.graph_chunk,
-                                     a.exchange if world > 1 else "rccl")
+                                     a.exchange if world > 1 else "rccl", settle_ms=a.clock_settle_ms)
 
     if world == 1 and not a.force_sharded and a.c1_leg:
         # BASELINE configs[0] ("Bivariate M1, Abe 1/10 CDNOW subset, 4000 iters on CPU numpy reference
         # path"): the same 4-chain c1 sampler on the GPU (2,000 sweeps after 80), next to its 1-core
         # CPU leg in cpu_baseline["c1"]
-        extra["c1"] = measure_config("c1", 1, rank, local_rank, None, 2000, 80, 0, "rccl", stored_phase=False)
+        extra["c1"] = measure_config("c1", 1, rank, local_rank, None, 2000, 80, 0, "rccl", stored_phase=False,
+                                     settle_ms=a.clock_settle_ms)
 
     if rank == 0:
         cpu = None
@@ -553,6 +579,7 @@ def main():
                          "every rank's IPC-mapped mail over xGMI (no host collective per sweep)") if p2p else
                         f"torch.cuda graph replay ({a.graph_chunk} sweeps: sweep + group kernels, RCCL all_gather, "
                         "level-2 kernel)" if a.graph_chunk else "eager: sweep + group kernels, RCCL all_gather, level-2"),
+            clock_settle_ms=round(settle_s * 1e3, 1),  # GPU busy with unrelated work before the warm-up
             roofline=roofline, cpu_baseline=cpu,
             host_us=(dict(host_us, clv_run_total=round(sum(host_us.values()), 3), timed_region=round(dt * 1e6, 3))
                      if host_us else None),

@@ -29,10 +29,28 @@ def main():
     s.run(5)
     s.synchronize()
     rows = {}
-    for case in ("cold", "after_long"):
+    cases = os.environ.get("CASES", "cold,after_long").split(",")
+    # after_busy: 2,000 sweeps' worth of unrelated GPU work (fp64 matmuls) then the driver's 5
+    # warm-up sweeps -- the GPU's clocks warm, the sampler's caches as cold as in "cold";
+    # long_then_idle: 2,000 sweeps then 0.2 s idle then 5 sweeps -- the caches warm, the clocks
+    # after the same idle gap as "cold"
+    a = torch.randn(2048, 2048, dtype=torch.float64, device="cuda:0")
+    for case in cases:
         for r in range(reps):
             if case == "after_long":
                 s.run(2000)
+            elif case == "after_busy":
+                b = a
+                t_end = time.perf_counter() + 0.021
+                while time.perf_counter() < t_end:
+                    b = torch.tanh(a @ b * 1e-3)
+                    torch.cuda.synchronize()
+                s.run(5)
+            elif case == "long_then_idle":
+                s.run(2000)
+                s.synchronize()
+                time.sleep(0.2)
+                s.run(5)
             else:
                 time.sleep(0.2)  # the driver's command: seconds of host work before the timed step
                 s.run(5)
