@@ -881,6 +881,31 @@ __device__ __forceinline__ void hyper_variates(const HyperArgs& a, int c, int64_
 template <int NS, int NT>
 __device__ __forceinline__ void hyper_sum_units(const HyperArgs& a, int c, const double* units, double (&acc)[NS]) {
   const Geometry& g = a.g;
+  // (every default plan: <= 512 units) both units' loads issued together, then added in the loop's
+  // order: one memory round trip instead of one per unit.  Small NS only: the 2 NS values in
+  // flight must not raise the sweep kernel's registers (trivariate K = 9: NS = 34, 125 -> 161 VGPRs)
+  if (NS <= 16 && g.n_units_global <= 2 * NT) {
+    const int u0 = threadIdx.x, u1 = threadIdx.x + NT, upr = g.units_per_rank;
+    const bool h0 = u0 < g.n_units_global, h1 = u1 < g.n_units_global;
+    const int64_t cs = (int64_t)g.stride * upr;
+    const double* p0 = units + ((int64_t)(u0 / upr) * g.n_chains + c) * cs + (u0 % upr);
+    const double* p1 = units + ((int64_t)(u1 / upr) * g.n_chains + c) * cs + (u1 % upr);
+    const double* q0 = h0 ? p0 : units;  // lanes without a unit read unit 0 and discard it
+    const double* q1 = h1 ? p1 : units;
+    double v0[NS], v1[NS];
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+      v0[j] = __hip_atomic_load(q0 + (int64_t)j * upr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      v1[j] = __hip_atomic_load(q1 + (int64_t)j * upr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+      acc[j] = 0.0;
+      if (h0) acc[j] += v0[j];
+      if (h1) acc[j] += v1[j];
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < NS; ++j) acc[j] = 0.0;
   for (int64_t u = threadIdx.x; u < g.n_units_global; u += NT) {
@@ -954,6 +979,51 @@ template <int D, int K, bool REPLAY, int NS, int NT>
 __device__ void hyper_body(const HyperArgs& a, int c, int64_t s, int mode, const double* units,
                            double (*red)[NS], double* tot, double* var_iw, double* var_chi, double* var_noise,
                            L2Scratch* l2) {
+  if constexpr (NS <= 16) {  // (trivariate / large K: the registers of the batch raised the
+                             // sweep kernel's allocation, K = 9 125 -> 159 VGPRs; the phases below)
+  // every load of the draw issued back to back — the prior block, the precomputed / replayed
+  // variates and this lane's unit partials — then the LDS staging: one memory round trip for all
+  // of them (hyper_variates' staging waits for its own loads before the units' are issued)
+  const int tid = threadIdx.x;
+  const int64_t hs = (D == 2) ? s + 1 : s;
+  static_assert(NT >= 198, "one prior element per lane");
+  const double pr = tid < 198 ? a.V[tid] : 0.0;
+  double w_iw = 0.0, w_chi = 0.0, w_noise = 0.0;
+  const bool preloaded = REPLAY || a.hvar;
+  if constexpr (REPLAY) {
+    const double* tv = a.r.tape + ((int64_t)c * a.r.tape_sweeps + (hs - 1)) * a.r.tape_sweep_stride +
+                       (a.r.tape_sweep_stride - TAPE_HYPER);
+    if (tid < 3) w_iw = tv[tid];
+    if (tid < 3) w_chi = tv[3 + tid];
+    if (tid < D * K) w_noise = tv[6 + tid];
+  } else if (a.hvar) {  // precomputed by this sweep's kernel (sc1 stores: read with sc1 loads)
+    const double* hv = a.hvar + (int64_t)c * HV;
+    if (tid < 3) w_iw = __hip_atomic_load(hv + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid < 3) w_chi = __hip_atomic_load(hv + 3 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid < D * K) w_noise = __hip_atomic_load(hv + 8 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  double acc[NS];
+  hyper_sum_units<NS, NT>(a, c, units, acc);
+  if (tid < 198) l2->prior[tid] = pr;  // published by block_reduce's barriers
+  if (preloaded) {
+    if (tid < 3) var_iw[tid] = w_iw;
+    if (tid < 3) var_chi[tid] = w_chi;
+    if (tid < D * K) var_noise[tid] = w_noise;
+  } else {
+    uint32_t k0, k1;
+    chain_key(a.r.seed, (int64_t)a.r.chain_first + c, &k0, &k1);
+    constexpr int NTRIL = D * (D - 1) / 2;
+    if (tid < NTRIL) var_iw[tid] = hyper_normal(k0, k1, HSLOT_NORMAL0 + tid, (uint32_t)hs);
+    if (tid >= 32 && tid < 32 + D * K)
+      var_noise[tid - 32] = hyper_normal(k0, k1, HSLOT_BETA_NORMAL0 + (tid - 32), (uint32_t)hs);
+    if (tid >= 64 && tid < 64 + D) {  // second wavefront: the gamma rejection loops
+      const int q = tid - 64;
+      var_chi[q] = chi2_draw(k0, k1, (uint32_t)hs, q, a.nu_n - D + 1 + q);
+    }
+  }
+  hyper_finish<D, K, REPLAY, NS, NT>(a, c, s, mode, acc, red, tot, var_iw, var_chi, var_noise, l2);
+  return;
+  }
   hyper_variates<D, K, REPLAY>(a, c, s, var_iw, var_chi, var_noise, l2);
   double acc[NS];
   hyper_sum_units<NS, NT>(a, c, units, acc);
