@@ -28,7 +28,7 @@
 #define CLV_L2_OPAQUE(P) (P)          // level-2 lane bookkeeping recomputed per sweep (not hoisted)
 #endif
 #ifndef CLV_L2_LANE0_MAX
-#define CLV_L2_LANE0_MAX 6  // persistent kernel (world size 1): one-lane level-2 algebra up to K*D (c3, K*D = 9: the element-parallel form 15.31 -> 15.11 us)
+#define CLV_L2_LANE0_MAX 6  // every level-2 draw (persistent kernel, fused tail, hyper kernel): one-lane algebra up to K*D (c3, K*D = 9: the element-parallel form 15.31 -> 15.11 us)
 #endif
 #ifndef PERSIST_REDUCE_GEN
 #define PERSIST_REDUCE_GEN 1  // persistent kernel: statistics formed chunk-wise in the reduction
@@ -930,7 +930,9 @@ __device__ void hyper_finish(const HyperArgs& a, int c, int64_t s, int mode, dou
   // algebra (element-parallel phases + one-lane core) and outputs
   if (tid == 0) CLV_STAMP(a.stamps, s, 6, false);
   L2Scratch* sc = l2;
-  level2_draw<D, K>(tot, var_iw, var_chi, var_noise, REPLAY, sc);
+  // (one-lane algebra up to K*D = 6 as in the persistent kernel: the element-parallel form at c4,
+  // K*D = 10, measured 84.4 -> 83.7 us per sweep against the one-lane one; the same bits)
+  level2_draw<D, K, CLV_L2_LANE0_MAX>(tot, var_iw, var_chi, var_noise, REPLAY, sc);
 #ifdef CLV_STAMP_L2SPLIT  // diagnostic: slot 5 = the level-2 draw's end (before finalize_hyper)
   if (tid == 0) CLV_STAMP(a.stamps, s, 5, false);
 #endif
