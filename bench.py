@@ -2,26 +2,31 @@
 """bench.py — MCMC customer-sweeps/s of the HIP sampler on MI355X (BASELINE.json metric).
 
 One step = one sweep (z, tau, level-2 draw, 20 MH steps, storage) of every chain over every
-customer.  N=1 workload = BASELINE.json configs[1] ("c2"): bivariate M2 on the full CDNOW CBS
-(23,570 customers, covariate first_sales_scaled), 4 chains, burnin 10000 / mcmc 10000 / thin 10,
-seed 42, 20 MH steps.  --gpus N > 1 (launched by torch.distributed.run, one rank per GPU) is
-weak scaling: every rank holds one 23,570-customer CDNOW copy of a N x 23,570-customer problem
-and the ranks exchange the level-2 sufficient statistics once per sweep: by default (--exchange
-auto) the persistent kernel of each rank stores its unit partials into every rank's IPC-mapped
-mail over xGMI (after a bitwise check against the RCCL path), else one RCCL all_gather per sweep.
+customer.  The primary workload is a BASELINE configuration at every N:
+  N = 1   configs[1] "c2": bivariate M2 on the full CDNOW CBS (23,570 customers, covariate
+          first_sales_scaled), 4 chains, burnin 10000 / mcmc 10000 / thin 10, seed 42, 20 MH steps;
+  N > 1   configs[4] "c5": trivariate M2, synthetic, 1.25M customers per GPU with 8 covariates
+          (weak scaling: 10M customers at N = 8), one process per GPU (torch.distributed.run),
+          sharded over the ranks with one exchange of the level-2 statistics per sweep (the fused
+          peer exchange over xGMI, verified bitwise against the RCCL all-gather path, else RCCL).
+The other BASELINE configurations run as `configs` legs (N = 1: c3, c4, c5 and c1; N > 1: c4
+strong scaling, and c2 tiled once per rank, labelled non-BASELINE), each with its own roofline
+(and bound evidence), c2 / c3 / c4 / c5 with a stored-sweep sub-line, c2 / c3 with the drop-in's
+whole BASELINE run timed end to end through mcmc_draw_parameters (run_mcmc_abe.py:60-77).
 
-Prints ONE JSON line (rank 0).  value = chains * customers * steps / wall time of the timed
-region (world size 1: one persistent-kernel launch when the grid fits at once, else hipGraph
-replay of the fused sweep launches; max over ranks).  roofline: the dominant kernel's algorithmic
-bytes per launch / its launch duration, measured with HIP start/stop events — for the persistent
-kernel on the timed region's own launch; for launch-per-sweep paths on the launches of a second
-pass over further sweeps of the same run (per-launch events force host-issued launches, so that
-pass gives kernel durations, not `value`); traffic from the committed rocprofv3 PMC summary.  cpu_baseline: the bitwise-pinned numpy restatement of
-the reference (oracle/ref_cpu.py) on 1 core.
+Prints ONE JSON line (rank 0).  value = chains * customers * steps / wall time of the timed region
+(max over ranks).  roofline: the dominant kernel's algorithmic bytes (SURVEY §8d per (chain,
+customer) sweep) per launch / its launch duration measured with HIP events on the sampler's stream
+— for the persistent kernel on the timed region's own launch; for launch-per-sweep paths on a pass
+over further sweeps (per-launch events), with measured traffic and the counters of the committed
+rocprofv3 summaries (profiles/).  cpu_baseline: the bitwise-pinned numpy restatement of the
+reference (oracle/ref_cpu.py) on 1 core (c2, and c1 / c3 under configs).
 """
 from __future__ import annotations
 
 import argparse
+import contextlib
+import io
 import json
 import os
 import subprocess
@@ -37,19 +42,46 @@ WORKLOADS = {
     # name: (D, data, covariates, chains, burnin, mcmc, thin, draw_sink)   (SURVEY.md §8 notation)
     "c1": (2, "abe", [], 4, 10000, 4000, 1, "full"),                      # run_mcmc_abe.py:61-71
     "c2": (2, "full", ["first_sales_scaled"], 4, 10000, 10000, 10, "full"),  # BASELINE configs[1]
-    "c3": (3, "full", ["gender_F", "age_scaled"], 4, 10000, 10000, 10, "full"),
+    "c3": (3, "full", ["gender_F", "age_scaled"], 4, 10000, 10000, 10, "full"),  # configs[2]
     # synthetic: 1M customers K=5 bivariate; 1.25M customers per GPU K=9 trivariate
     "c4": (2, "synthetic:1000000:5:20250718", ["c1", "c2", "c3", "c4"], 1, 5000, 5000, 1, "summary"),
     "c5": (3, "synthetic:1250000:9:20250719", [f"c{k}" for k in range(1, 9)], 1, 5000, 5000, 1, "summary"),
 }
+BASELINE_INDEX = {"c1": 0, "c2": 1, "c3": 2, "c4": 3, "c5": 4}
+
+
+def primary_workload(world: int) -> str:
+    """The BASELINE configuration the line's `value` is quoted on: c2 on one GPU (configs[1]); the
+    8-GPU weak-scaling run c5 (configs[4], 1.25M customers per GPU) at N > 1 (verdict r4 #7)."""
+    return "c2" if world == 1 else "c5"
+
+
+def config_legs(world: int, primary: str):
+    """The `configs` legs: every other BASELINE configuration at this N (c1 and c3 are one-GPU
+    configurations; at N > 1 c2 runs tiled once per rank, a non-BASELINE rehearsal of the
+    CDNOW-size exchange)."""
+    if world == 1:
+        return [c for c in ("c3", "c4", "c5") if c != primary]
+    return [c for c in ("c4", "c2") if c != primary]
+
+
+def survey_bytes(D: int, K: int, stored_frac: float, draw_sink: str) -> float:
+    """SURVEY §8d's algorithmic HBM bytes per (chain, customer) sweep: read x 4, t_x 8, T 8,
+    8 (K-1) covariates, (D = 3) log_s 8, 8 D of state; write 8 D of state; per stored sweep the
+    8 (D+2) B level-1 draw (full sink) or +0 (summary sinks), amortised by `stored_frac`.
+    c1 84 (thin 1), c2 60 + 3.2, c3 92 + 4.0, c4 84, c5 140."""
+    rd = 4 + 8 + 8 + 8 * (K - 1) + (8 if D == 3 else 0) + 8 * D
+    wr = 8 * D
+    per_store = 8.0 * (D + 2) if draw_sink == "full" else 0.0
+    return rd + wr + per_store * stored_frac
 
 
 def algorithmic_bytes(D: int, K: int, stored_frac: float, draw_sink: str) -> float:
-    """HBM bytes one (chain, customer) moves per sweep in the sweep kernel:
-    read x (4) + t_x, T (16) + K-1 covariates (8 each) + log_s (D=3: 8) + lambda, mu (16);
-    write lambda, mu (16); per stored sweep (share `stored_frac`): the level-1 draw 8(D+2)
-    (full sink) or the read-modify-write of 9 (D=2) / 11 (D=3) running sums (summary sinks; plus
-    the float32 (lambda, mu) pair, 8, for "summary+pct")."""
+    """The sweep kernel's own streaming bytes per (chain, customer) sweep: as
+    survey_bytes but with the carried state only (lambda, mu: 16 B each way — eta is redrawn from
+    its conjugate posterior every sweep, tri:306-333, never read back), and on stored sweeps of the
+    summary sinks the read-modify-write of 9 (D=2) / 11 (D=3) running sums (+ the float32
+    (lambda, mu) pair for "summary+pct")."""
     rd = 4 + 16 + 8 * (K - 1) + (8 if D == 3 else 0) + 16
     wr = 16
     if draw_sink == "full":
@@ -66,19 +98,23 @@ def _kernel_matches(name: str, kname: str, D: int, K: int) -> bool:
     return kname in name and f"<{D}, {K}," in name
 
 
-def committed_traffic(workload: str, sharded: bool, kname: str = "sweep_kernel", D: int = 0, K: int = 0):
-    """HBM bytes per sweep-kernel launch from the committed rocprofv3 PMC summary of this workload
-    (profiles/*_summary.json written by tools/summarize_profile.py): FETCH_SIZE and WRITE_SIZE
-    corrected by the calibration kernels of tools/calib_fetch.hip; None if absent."""
+def _summaries(workload: str):
     import glob
-    if sharded:
-        return None
-    best = None
+    out = []
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{workload}_*summary.json"))):
         try:
-            d = json.load(open(path))
+            out.append((path, json.load(open(path))))
         except Exception:
             continue
+    return out
+
+
+def committed_traffic(workload: str, kname: str, D: int, K: int):
+    """HBM bytes per sweep of the workload's kernel from the latest committed rocprofv3 PMC summary
+    (profiles/r*_<workload>_*summary.json, tools/summarize_profile.py): FETCH_SIZE and WRITE_SIZE
+    corrected by the calibration of tools/calib_fetch.hip; None if absent."""
+    best = None
+    for path, d in _summaries(workload):
         for name, k in d.get("kernels", {}).items():
             if _kernel_matches(name, kname, D, K) and "traffic_bytes" in k:
                 best = dict(bytes_per_sweep=k["traffic_bytes"] / k.get("sweeps_per_dispatch", 1),
@@ -92,20 +128,13 @@ N_SIMDS = 1024  # 256 CUs x 4 SIMDs (MI355X_MICROARCH.md)
 N_XCDS = 8      # GRBM_GUI_ACTIVE is summed over the 8 XCDs
 
 
-def committed_counters(workload: str, sharded: bool, kname: str = "sweep_kernel", D: int = 0, K: int = 0):
-    """Counter evidence for the roofline's `bound` from the committed rocprofv3 summary of this
-    workload (tools/summarize_profile.py): VALU busy = SQ_ACTIVE_INST_VALU (quad-cycles, x4) summed
-    over the kernel's waves / (1,024 SIMDs x the dispatch's cycles, GRBM_GUI_ACTIVE / 8 XCDs) — the
-    share of SIMD cycles issuing VALU work — and the VALU-active share of the waves' lifetime."""
-    import glob
-    if sharded:
-        return None
+def committed_counters(workload: str, kname: str, D: int, K: int):
+    """Counter evidence for the roofline's `bound` from the latest committed rocprofv3 summary of the
+    workload: VALU busy = SQ_ACTIVE_INST_VALU (quad-cycles, x4) summed over the kernel's waves /
+    (1,024 SIMDs x the dispatch's cycles, GRBM_GUI_ACTIVE / 8 XCDs) — the share of SIMD cycles
+    issuing VALU work — and the VALU-active share of the waves' lifetime."""
     best = None
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{workload}_*summary.json"))):
-        try:
-            d = json.load(open(path))
-        except Exception:
-            continue
+    for path, d in _summaries(workload):
         for name, k in d.get("kernels", {}).items():
             if _kernel_matches(name, kname, D, K) and "valu_active_quadcycles_per_wave" in k and k.get("grbm_gui_active"):
                 cycles = k["grbm_gui_active"] / N_XCDS
@@ -117,8 +146,11 @@ def committed_counters(workload: str, sharded: bool, kname: str = "sweep_kernel"
     return best
 
 
+BOUND_RULE = "hbm if measured HBM traffic >= 0.6 of peak; else valu if VALU busy >= 0.7; else latency"
+
+
 def load_workload(name: str, world: int = 1):
-    """CBS of a workload.  CDNOW: the committed CBS columns (weak scaling: one copy per rank).
+    """CBS of a workload.  CDNOW: the committed CBS columns (N > 1: one copy per rank).
     Synthetic: mcmc_clv_model_amd.data.synthetic_cbs with n per GPU (c5 weak scaling: n x world)."""
     import numpy as np
     import pandas as pd
@@ -149,8 +181,7 @@ def cpu_baseline_child(workload: str, warm: int, timed: int) -> None:
     from oracle import ref_cpu as orc
     df, D, covs, chains, burnin, mcmc, thin, sink = load_workload(workload)
     cbs, X = orc.design_matrix(df, covs)
-    K = X.shape[1]
-    hyper = orc.default_hyper(K, D)
+    hyper = orc.default_hyper(X.shape[1], D)
     stamps = {}
 
     def on_sweep(step):
@@ -171,6 +202,8 @@ def cpu_baseline_child(workload: str, warm: int, timed: int) -> None:
 
 
 def cpu_baseline(workload: str, warm: int = 20, timed: int = 200, parallel: bool = True):
+    """the oracle on 1 core (c1 / c2 / c3: >= 200 timed sweeps after 20; c4 / c5: 5
+    after 2), and with `parallel` an all-cores throughput (P single-threaded chains at once)."""
     if WORKLOADS[workload][1].startswith("synthetic:"):  # ~3 s/sweep on one core (SURVEY §6)
         warm, timed = 2, 5
     env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1",
@@ -225,108 +258,258 @@ def settle_clocks(ms: float, device: int) -> float:
     return time.perf_counter() - t0
 
 
-def measure_config(name: str, world: int, rank: int, local_rank: int, dist, steps: int, warmup: int,
-                   graph_chunk: int, exchange: str, stored_phase: bool = True, settle_ms: float = 0.0) -> dict:
-    """One BASELINE multi-GPU configuration at this world size: c4 = 1M bivariate
-    customers K=5 sharded over the ranks (strong scaling: the same problem at every N), c5 = 1.25M
-    trivariate customers K=9 per rank (weak scaling).  Wall time of `steps` sweeps (max over ranks)
-    after `warmup` sweeps; HBM fraction of the algorithmic bytes against N x 8 TB/s.  With
-    `stored_phase` (and a burn-in longer than the window) the same chains then continue past the
-    burn-in and `steps` stored sweeps are timed too (`stored`: each also read-modify-writes the
-    customer's running sums), and `whole_run` combines both phases' per-sweep times over the
-    BASELINE run's burn-in + mcmc sweeps."""
+def roofline_for(workload: str, kname: str, D: int, K: int, bpu: float, units: int, t_launch: float, spl: int,
+                 sharded: bool, **extra) -> dict:
+    """The roofline object of one kernel: SURVEY §8d bytes x (chain, customer) sweeps per launch /
+    the launch's duration, measured traffic and the counters that decide `bound` (committed
+    rocprofv3 summaries of this workload's instance; none for sharded runs, profiled at N = 1)."""
+    achieved = bpu * units / t_launch / 1e9
+    r = dict(bound=None, achieved=round(achieved, 3), peak=HBM_PEAK_GBS, unit="GB/s",
+             frac=round(achieved / HBM_PEAK_GBS, 6), traffic=None, bytes_per_unit=round(bpu, 3),
+             units_per_launch=units, sweeps_per_launch=spl, launch_us=round(t_launch * 1e6, 3),
+             sweep_kernel_us=round(t_launch / spl * 1e6, 3), **extra)
+    tr = None if sharded else committed_traffic(workload, kname, D, K)
+    if tr:  # HBM bytes per launch (calibrated PMC), per sweep x sweeps per launch
+        r["traffic"] = round(tr["bytes_per_sweep"] * spl)
+        r["traffic_source"] = f"{tr['source']}: {tr['counters']}"
+    ev = (None if sharded else committed_counters(workload, kname, D, K)) or {}
+    if r["traffic"] is not None:
+        ev["hbm_traffic_frac"] = round(r["traffic"] / t_launch / 1e9 / HBM_PEAK_GBS, 4)
+    if ev.get("hbm_traffic_frac", 0.0) >= 0.6:
+        r["bound"] = "hbm"
+    elif ev.get("valu_busy_frac", 0.0) >= 0.7:
+        r["bound"] = "valu"
+    elif "valu_busy_frac" in ev:
+        r["bound"] = "latency"
+    else:
+        r["bound"] = "unmeasured"
+    ev["rule"] = BOUND_RULE
+    r["bound_evidence"] = ev
+    return r
+
+
+def whole_run_e2e(name: str, reps: int = 2) -> dict:
+    """The drop-in's BASELINE run end to end, as the reference's driver times it (run_mcmc_abe.py:60-77:
+    wall time around mcmc_draw_parameters, trace 1000): upload, every sweep of burn-in + mcmc, every
+    stored draw returned in numpy arrays (the reference's layout).  `reps` calls; the first one also
+    pays one-time process costs (copy-pool threads, pinned staging)."""
+    import numpy as np
+    from mcmc_clv_model_amd import mcmc_draw_parameters, mcmc_draw_parameters_rfm_m
+    df, D, covs, chains, burnin, mcmc, thin, sink = load_workload(name)
+    fn = mcmc_draw_parameters if D == 2 else mcmc_draw_parameters_rfm_m
+    walls = []
+    nbytes = 0
+    for _ in range(reps):
+        out = io.StringIO()
+        t0 = time.perf_counter()
+        with contextlib.redirect_stdout(out):
+            d = fn(df, covs, mcmc=mcmc, burnin=burnin, thin=thin, chains=chains, seed=42, trace=1000, n_mh_steps=20)
+        walls.append(time.perf_counter() - t0)
+        nbytes = int(sum(a.nbytes for a in d["level_1"]))
+        ok = bool(np.isfinite(d["log_likelihood"]))
+        del d  # (freeing the 3 GB result is not the next call's cost)
+    best = min(walls[1:]) if len(walls) > 1 else walls[0]
+    n = len(df)
+    return dict(value=chains * n * (burnin + mcmc) / best, unit="customer-sweeps/s", seconds=round(best, 4),
+                first_call_seconds=round(walls[0], 4), calls=reps, level1_bytes=nbytes, finite=ok,
+                sweeps=f"{burnin} burn-in + {mcmc} (thin {thin}), {chains} chains",
+                note="mcmc_draw_parameters%s end to end, draws returned (trace 1000, stdout captured)"
+                     % ("" if D == 2 else "_rfm_m"))
+
+
+def run_leg(name: str, world: int, rank: int, local_rank: int, dist, steps: int, warmup: int, *,
+            graph_chunk: int = 32, exchange: str = "rccl", settle_ms: float = 0.0, stored_phase: bool = True,
+            timing_steps: int = 3000, force_sharded: bool = False, phase: str = "burnin", blocks_per_unit: int = 0,
+            one_call_warmup: bool = False, cold: bool = False, host_split: bool = False) -> dict:
+    """One BASELINE configuration at this world size: `warmup` untimed sweeps, then exactly `steps`
+    timed sweeps bracketed by barrier + synchronize (wall time, max over ranks).  The roofline
+    comes from HIP events on the sampler's stream: the timed launch itself (persistent kernel) or a
+    pass of min(steps, timing_steps) further sweeps (launch-per-sweep).  With `stored_phase` (and a
+    burn-in longer than the window) the same chains continue 100 sweeps past the burn-in and
+    `steps` stored sweeps are timed as well (bi:402-428: the draws or the running sums);
+    `whole_run` combines both phases' per-sweep times over the BASELINE run's burn-in + mcmc
+    (c4 / c5; c2 / c3 measure the drop-in end to end instead, see whole_run_e2e)."""
     import torch
     from mcmc_clv_model_amd.sampler import HipSampler, build_problem
     df, D, covs, chains, burnin, mcmc, thin, sink = load_workload(name, world)
+    if phase == "stored":
+        mcmc, burnin = mcmc + burnin, 0
+    K = len(covs) + 1
     n_total = len(df)
+    mcmc_workload = mcmc
+    sharded = world > 1 or force_sharded
     p = build_problem(df, covs, D)
     del df
-    mcmc0 = mcmc
-    mcmc = max(mcmc, warmup + steps - burnin, 100 + steps)
-    if world == 1:
+    if not sharded:
         kern = HipSampler(p, mcmc=mcmc, burnin=burnin, thin=thin, chains=chains, seed=42, draw_sink=sink,
-                          device=local_rank)
+                          device=local_rank, blocks_per_unit=blocks_per_unit)
         run, sync = kern.run, kern.synchronize
     else:
         from mcmc_clv_model_amd.distributed import ShardedSampler
         kern = ShardedSampler(p, rank=rank, world=world, chains=chains, mcmc=mcmc, burnin=burnin, thin=thin, seed=42,
-                              draw_sink=sink, device=local_rank, graph_chunk=graph_chunk, exchange=exchange,
-                              verify_sweeps=8)
+                              draw_sink=sink, device=local_rank, graph_chunk=graph_chunk,
+                              exchange=exchange if world > 1 else "rccl", verify_sweeps=8)
         run, sync = kern.step, kern.synchronize
     del p
+    info = kern.launch_info()
+    persistent = info["persistent"]
+    p2p = sharded and getattr(kern, "exchange", None) == "p2p"
+    kname = "persist_kernel" if persistent else "sweep_kernel"
+    n_local = kern.n
 
-    def timed(n: int) -> float:
-        """Wall time of n sweeps bracketed by barrier + synchronize, max over ranks."""
+    def timed(n: int, events: bool):
+        """Wall time of n sweeps bracketed by barrier + synchronize (max over ranks); with `events`
+        (persistent kernel) also the timed launch's duration from its HIP events."""
+        if events:
+            kern.set_timing(True)
         if dist:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         run(n)
-        sync()
+        if sharded:
+            sync()
         torch.cuda.synchronize()
         if dist:
             dist.barrier()
         dt = time.perf_counter() - t0
+        kt = None
+        if events:
+            kt = kern.kernel_time()
+            kern.set_timing(False)
         if dist:
             t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local_rank}")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dt = float(t.item())
-        return dt
+        return dt, kt
 
-    settle_clocks(settle_ms, local_rank)  # (the problem build above left the GPU idle for seconds)
-    run(warmup)
+    def launch_roofline(first: int, n_t: int, kt, events_note: str):
+        """Roofline of n_t sweeps starting at sweep `first` (persistent: kt of the timed launch)."""
+        if kt is None:  # launch-per-sweep: event-timed pass over further sweeps of the same chains
+            kern.set_timing(True)
+            run(n_t)
+            sync()
+            kt = kern.kernel_time()
+            kern.set_timing(False)
+        if not kt or not kt["sweep_launches"]:
+            return None
+        t_sweep = kt["sweep_ms"] / kt["sweep_launches"] * 1e-3
+        spl = n_t if persistent else 1  # sweeps per launch
+        frac = stored_fraction(burnin, thin, first, first + n_t - 1)
+        r = roofline_for(name, kname, D, K, survey_bytes(D, K, frac, sink), chains * n_local * spl, t_sweep * spl, spl,
+                         sharded and not p2p,
+                         kernel=(("persist_kernel (one launch for all sweeps of a clv_run; level-2 workgroup per "
+                                  "chain" + ("; unit partials exchanged over xGMI" if p2p else "") + ")")
+                                 if persistent else
+                                 ("sweep_kernel (incl. fused level-2 tail" +
+                                  ("; unit partials exchanged through the peers' mail" if p2p else "") + ")")
+                                 if (not sharded or p2p) else "sweep_kernel"),
+                         bytes_per_unit_kernel=round(algorithmic_bytes(D, K, frac, sink), 3),
+                         bytes_note="bytes_per_unit: SURVEY §8d (per stored sweep the full sink's draw, summary "
+                                    "sinks +0); bytes_per_unit_kernel: the kernel's own streaming bytes",
+                         timed_launches=kt["sweep_launches"] // spl, events=events_note)
+        if kt.get("hyper_launches"):
+            r["hyper_kernel_us"] = round(kt["hyper_ms"] / kt["hyper_launches"] * 1e3, 3)
+        return r
+
+    settle_s = settle_clocks(settle_ms, local_rank)  # (the problem build left the GPU idle for seconds)
+    if persistent and one_call_warmup:  # the warm-up steps one call each, through the timed path (events
+        kern.set_timing(True)           # on): the timed call is not the process's first of its kind
+        for _ in range(warmup):
+            run(1)
+            sync()
+            torch.cuda.synchronize()
+        kern.kernel_time()
+        kern.set_timing(False)
+    else:
+        run(warmup)
     sync()
-    dt = timed(steps)  # burn-in sweeps warmup+1 .. warmup+steps
-    # the stored phase (verdict r3: half of the BASELINE run; every sweep after burn-in
-    # read-modify-writes the customer's running sums, bi:402-428): continue the same chains into
-    # it, 100 sweeps past the boundary (warm), then time `steps` stored sweeps
-    phases = None
-    K = len(covs) + 1
-    kname = "sweep_kernel"  # (c4 / c5: launch-per-sweep; the committed profiles are of that kernel)
-
-    def traffic(tag):  # calibrated PMC bytes per (chain, customer) sweep from the committed profile
-        tr = committed_traffic(tag, False, kname, D, K) if world == 1 else None
-        return None if not tr else dict(bytes_per_unit=round(tr["bytes_per_sweep"] / (chains * n_total), 2),
-                                        source=tr["source"])
-    if stored_phase and burnin > warmup + steps:
-        done = warmup + steps
+    dt, kt = timed(steps, persistent)
+    host_us = kern.host_times() if (host_split and persistent and not sharded) else None
+    value = chains * n_total * steps / dt
+    roof = launch_roofline(warmup + 1, steps if persistent else min(steps, timing_steps), kt,
+                           "the timed region's launch" if persistent else
+                           f"a pass of {min(steps, timing_steps)} further sweeps, one event pair per launch")
+    done = warmup + steps + (0 if persistent else min(steps, timing_steps))
+    res = dict(workload=f"{name}: {'bivariate' if D == 2 else 'trivariate'}, K={K}, " +
+                        ("synthetic (mcmc_clv_model_amd.data.synthetic_cbs)" if WORKLOADS[name][1].startswith("synthetic:")
+                         else f"CDNOW {WORKLOADS[name][1]} CBS"),
+               baseline_config=BASELINE_INDEX[name],
+               scaling="strong" if name == "c4" else "weak", value=value, unit="customer-sweeps/s",
+               n_customers=n_total, customers_per_gpu=n_total // world, chains=chains, steps=steps, warmup=warmup,
+               ms_per_step=dt / steps * 1e3, draw_sink=sink, burnin=burnin, mcmc=mcmc_workload, thin=thin,
+               roofline=roof,
+               path=("persistent kernel" if persistent else "launch-per-sweep sweep kernel") +
+                    ("" if not sharded else
+                     (", unit partials stored into every rank's mail over xGMI by the kernel (no host collective)"
+                      if p2p else ", RCCL all-gather + level-2 kernel per sweep") +
+                     (f" ({kern.p2p_note})" if getattr(kern, "p2p_note", None) else "")),
+               phase=f"burn-in (sweeps {warmup + 1}..{warmup + steps})" if phase == "burnin" else
+                     f"stored (burn-in 0, sweeps {warmup + 1}..{warmup + steps})",
+               clock_settle_ms=round(settle_s * 1e3, 1))
+    if host_us:
+        res["host_us"] = dict(host_us, clv_run_total=round(sum(host_us.values()), 3), timed_region=round(dt * 1e6, 3))
+    if sharded:
+        res["exchange"] = dict(kind=getattr(kern, "exchange", None), note=getattr(kern, "p2p_note", None),
+                               requested=exchange if world > 1 else "rccl")
+    if cold and persistent and not sharded:
+        # ADVICE r4: the timed window above is steady state (clocks settled; the timed call leaves its
+        # last level-2 draw pending for the next call).  Here the same K sweeps from an idle GPU (0.3 s,
+        # no settle) with that draw included (flushed inside the timed region)
+        time.sleep(0.3)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        run(steps)
+        kern.flush()
+        torch.cuda.synchronize()
+        dtc = time.perf_counter() - t0
+        done += steps
+        res["cold"] = dict(ms_per_step=dtc / steps * 1e3, value=chains * n_total * steps / dtc,
+                           note="after 0.3 s of idle GPU, no clock settle, the deferred last level-2 draw "
+                                "flushed inside the timed region")
+    if stored_phase and burnin > done + steps:
+        # the stored phase (half of the BASELINE run; every stored sweep writes the draws or
+        # read-modify-writes the running sums, bi:402-428): the same chains 100 sweeps past the boundary
+        # (warm), then `steps` stored sweeps
         run(burnin + 100 - done)
         sync()
-        dt_st = timed(steps)
+        settle_clocks(settle_ms, local_rank)
+        dt_st, kt_st = timed(steps, persistent)
         first = burnin + 101
-        bpu_st = algorithmic_bytes(D, len(covs) + 1, stored_fraction(burnin, thin, first, first + steps - 1), sink)
+        n_st = steps if persistent else min(steps, timing_steps)
+        roof_st = launch_roofline(first, n_st, kt_st, "the timed stored launch" if persistent else
+                                  f"a pass of {n_st} further stored sweeps")
         v_st = chains * n_total * steps / dt_st
-        t_b, t_s = dt / steps, dt_st / steps  # s per sweep in each phase
-        whole = chains * n_total * (burnin + mcmc0) / (burnin * t_b + mcmc0 * t_s)
-        phases = dict(
-            stored=dict(value=v_st, ms_per_step=t_s * 1e3, sweeps=f"{first}..{first + steps - 1}",
-                        bytes_per_unit=round(bpu_st, 2),
-                        hbm_frac=round(bpu_st * v_st / 1e9 / (world * HBM_PEAK_GBS), 5),
-                        measured_traffic=traffic(f"{name}stored")),
-            whole_run=dict(value=whole, sweeps=f"{burnin} burn-in + {mcmc0} stored",
-                           note="customer-sweeps/s of the BASELINE run from the two phases' per-sweep times"))
-    linfo = kern.launch_info()
-    persistent = linfo["persistent"]
-    exch = getattr(kern, "exchange", None)
-    note = getattr(kern, "p2p_note", None)
+        fr = stored_fraction(burnin, thin, first, first + steps - 1)
+        b8 = survey_bytes(D, K, fr, sink)
+        bk = algorithmic_bytes(D, K, fr, sink)
+        res["stored"] = dict(value=v_st, ms_per_step=dt_st / steps * 1e3, sweeps=f"{first}..{first + steps - 1}",
+                             bytes_per_unit=round(b8, 2), hbm_frac=round(b8 * v_st / 1e9 / (world * HBM_PEAK_GBS), 5),
+                             bytes_per_unit_kernel=round(bk, 2),
+                             hbm_frac_kernel=round(bk * v_st / 1e9 / (world * HBM_PEAK_GBS), 5),
+                             bytes_note="bytes_per_unit / hbm_frac: SURVEY §8d (summary sinks +0 per stored sweep); "
+                                        "*_kernel: the kernel's own bytes incl. the running sums' read-modify-write",
+                             roofline=roof_st)
+        if WORKLOADS[name][1].startswith("synthetic:"):
+            t_b, t_s = dt / steps, dt_st / steps
+            res["whole_run"] = dict(value=chains * n_total * (burnin + mcmc_workload) / (burnin * t_b + mcmc_workload * t_s),
+                                    sweeps=f"{burnin} burn-in + {mcmc_workload} stored",
+                                    note="customer-sweeps/s of the BASELINE run from the two phases' per-sweep times")
+    b8 = survey_bytes(D, K, stored_fraction(burnin, thin, warmup + 1, warmup + steps), sink)
+    res["hbm_frac"] = round(b8 * value / 1e9 / (world * HBM_PEAK_GBS), 5)
+    res["bytes_per_unit"] = round(b8, 2)
+    res["_persistent"] = persistent
+    res["_p2p"] = p2p
+    res["_timed_region"] = (f"one persistent-kernel launch of {steps} sweeps" if persistent and not sharded else
+                            f"one persistent-kernel launch of {steps} sweeps per rank, unit partials stored into every "
+                            "rank's IPC-mapped mail over xGMI (no host collective per sweep)" if persistent else
+                            "hipGraph replay of fused sweep launches" + (
+                                " (unit partials exchanged through the peers' mail by the kernels)" if p2p else "")
+                            if (not sharded or p2p) else
+                            f"torch.cuda graph replay ({graph_chunk} sweeps: sweep + group kernels, RCCL all_gather, "
+                            "level-2 kernel)" if graph_chunk else "eager: sweep + group kernels, RCCL all_gather, level-2")
     kern.close()
-    value = chains * n_total * steps / dt
-    bpu = algorithmic_bytes(D, K, stored_fraction(burnin, thin, warmup + 1, warmup + steps), sink)
-    data = WORKLOADS[name][1]
-    return dict(workload=f"{name}: {'bivariate' if D == 2 else 'trivariate'}, K={K}, " +
-                         ("synthetic (mcmc_clv_model_amd.data.synthetic_cbs)" if data.startswith("synthetic:") else
-                          f"CDNOW {data} CBS"),
-                scaling="strong" if name == "c4" else "weak", value=value, unit="customer-sweeps/s",
-                n_customers=n_total, customers_per_gpu=n_total // world, chains=chains, steps=steps, warmup=warmup,
-                ms_per_step=dt / steps * 1e3, draw_sink=sink,
-                hbm_frac=round(bpu * value / 1e9 / (world * HBM_PEAK_GBS), 5), bytes_per_unit=round(bpu, 2),
-                path=("persistent kernel" if persistent else "launch-per-sweep sweep kernel") +
-                     ("" if world == 1 else
-                      (", unit partials stored into every rank's mail over xGMI by the kernel (no host collective)"
-                       if exch == "p2p" else ", RCCL all-gather + level-2 kernel per sweep") +
-                      (f" ({note})" if note else "")),
-                phase=f"burn-in (sweeps {warmup + 1}..{warmup + steps})", measured_traffic=traffic(name),
-                **(phases or {}))
+    return res
 
 
 def main():
@@ -334,21 +517,21 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=19000)
     ap.add_argument("--warmup", type=int, default=1000)
-    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default=None, choices=sorted(WORKLOADS),
+                    help="primary workload (default: c2 at N = 1, c5 at N > 1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-kernel-timing", action="store_true", help="skip the event-timed roofline pass")
     ap.add_argument("--timing-steps", type=int, default=3000, help="sweeps in the event-timed roofline pass")
     ap.add_argument("--graph-chunk", type=int, default=32,
-                    help="sharded path: sweeps (incl. the RCCL all-gather) per captured torch.cuda graph; 0 = eager")
+                    help="sharded RCCL path: sweeps (incl. the all-gather) per captured torch.cuda graph; 0 = eager")
     ap.add_argument("--force-sharded", action="store_true",
                     help="use the sharded path (torch.distributed exchange) even at world size 1")
     ap.add_argument("--exchange", default="auto", choices=["auto", "p2p", "rccl"],
-                    help="world size > 1: unit-partial exchange per sweep — p2p = persistent kernel storing into "
-                         "every rank's IPC-mapped mail over xGMI (auto: where it fits and verifies bitwise "
-                         "against RCCL), rccl = all_gather per sweep")
-    ap.add_argument("--scaling-configs", default="c4,c5",
-                    help="BASELINE multi-GPU configurations also measured at this N (c4 strong, c5 weak "
-                         "scaling), reported under `configs`; '' to skip")
+                    help="world size > 1: unit-partial exchange per sweep — p2p = the kernels store into every "
+                         "rank's IPC-mapped mail over xGMI (auto: where it verifies bitwise against RCCL), "
+                         "rccl = all_gather per sweep")
+    ap.add_argument("--scaling-configs", default=None,
+                    help="comma-separated `configs` legs (default: the other BASELINE configurations at this N); "
+                         "'' to skip")
     ap.add_argument("--scaling-steps", type=int, default=1000)
     ap.add_argument("--blocks-per-unit", type=int, default=0,
                     help="(world size 1, A/B) blocks per statistics unit instead of the plan's (0)")
@@ -357,6 +540,10 @@ def main():
                          "(the running sums' read-modify-write / the draws' stores of bi:402-428)")
     ap.add_argument("--no-c1-leg", dest="c1_leg", action="store_false",
                     help="skip BASELINE configs[0] (c1 on the GPU and its 1-core CPU leg)")
+    ap.add_argument("--no-stored-phase", dest="stored_phase", action="store_false",
+                    help="skip the stored-sweep sub-lines")
+    ap.add_argument("--no-whole-run", dest="whole_run", action="store_false",
+                    help="skip the drop-in's end-to-end BASELINE runs (c2 / c3 through mcmc_draw_parameters)")
     ap.add_argument("--one-gpu-rehearsal", action="store_true",
                     help="world size > 1 on a one-GPU box: every rank on device 0, gloo process group (the "
                          "exchange paths are exercised; the numbers are not a scaling measurement)")
@@ -368,10 +555,9 @@ def main():
     ap.add_argument("--cpu-timed", type=int, default=200)
     a = ap.parse_args()
     if a.cpu_baseline_child:
-        cpu_baseline_child(a.workload, a.cpu_warm, a.cpu_timed)
+        cpu_baseline_child(a.workload or "c2", a.cpu_warm, a.cpu_timed)
         return
 
-    import numpy as np
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -397,195 +583,86 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
 
     from mcmc_clv_model_amd import _lib
-    from mcmc_clv_model_amd.sampler import HipSampler, build_problem
-
-    df, D, covs, chains, burnin, mcmc, thin, sink = load_workload(a.workload, world)
+    _lib.lib()
+    name = a.workload or primary_workload(world)
+    exch = a.exchange if world > 1 else "rccl"
+    prim = run_leg(name, world, rank, local_rank, dist, a.steps, a.warmup, graph_chunk=a.graph_chunk, exchange=exch,
+                   settle_ms=a.clock_settle_ms, stored_phase=a.stored_phase, timing_steps=a.timing_steps,
+                   force_sharded=a.force_sharded, phase=a.phase, blocks_per_unit=a.blocks_per_unit,
+                   one_call_warmup=True, cold=True, host_split=True)
+    D, data, covs, chains, burnin, mcmc, thin, sink = WORKLOADS[name]
     if a.phase == "stored":
         mcmc, burnin = mcmc + burnin, 0
-    total = a.warmup + a.steps + (0 if a.no_kernel_timing else min(a.steps, a.timing_steps))
-    mcmc_workload = mcmc
-    mcmc = max(mcmc, total - burnin)  # draw buffers also cover the sweeps of the roofline pass
-    n_total = len(df)
-    if not sharded:
-        p = build_problem(df, covs, D)
-        s = HipSampler(p, mcmc=mcmc, burnin=burnin, thin=thin, chains=chains, seed=42, draw_sink=sink,
-                       device=local_rank, blocks_per_unit=a.blocks_per_unit)
-        run = s.run
-        sync = s.synchronize
-        kern = s
-    else:
-        from mcmc_clv_model_amd.distributed import ShardedSampler
-        p = build_problem(df, covs, D)
-        ss = ShardedSampler(p, rank=rank, world=world, chains=chains, mcmc=mcmc, burnin=burnin, thin=thin, seed=42,
-                            draw_sink=sink, device=local_rank, graph_chunk=a.graph_chunk,
-                            exchange=a.exchange if world > 1 else "rccl", verify_sweeps=8)
-        run = ss.step
-        sync = ss.synchronize
-        kern = ss
+    if world == 1 and not a.force_sharded and a.whole_run and name in ("c2", "c3") and a.phase == "burnin":
+        prim["whole_run"] = whole_run_e2e(name)
 
-    K = len(covs) + 1
-    timing = not a.no_kernel_timing
-    info = kern.launch_info()
-    persistent = info["persistent"]
-    one_launch = persistent   # all sweeps of a clv_run in one launch
-    p2p = sharded and persistent
-    # persistent kernel: the timed launch itself is bracketed by HIP start/stop events recorded on
-    # the sampler's stream (the launch's stream), inside the timed region; the warm-up sweeps run
-    # through that same path (events included, their times discarded), so the timed call is not
-    # the first of its kind in the process
-    live = timing and one_launch
-    settle_s = settle_clocks(a.clock_settle_ms, local_rank)
-    if live:
-        kern.set_timing(True)
-    if one_launch:  # the warm-up steps one call each: the host path of a call is warm when timed
-        for _ in range(a.warmup):
-            run(1)
-            sync()
-            torch.cuda.synchronize()
-    else:
-        run(a.warmup)
-    sync()
-    if live:
-        kern.kernel_time()
-        kern.set_timing(True)  # (counters reset: only the timed launch is harvested below)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    run(a.steps)                      # timed region: persistent launch / hipGraph replay / sharded steps
-    if sharded:
-        sync()                        # (HipSampler.run returns when its launches are done)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    host_us = kern.host_times() if (persistent and not sharded) else None  # where the step's host time went
-    kt_live = None
-    if live:
-        kt_live = kern.kernel_time()
-        kern.set_timing(False)
-    if dist:
-        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local_rank}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-    units = chains * n_total * a.steps
-    value = units / dt
-
-    # Launch-per-sweep paths: a roofline pass continues the same sweeps with HIP start/stop events
-    # on every sweep launch (hipExtLaunchKernelGGL: the dispatch's own timestamps).  Launches are
-    # then host-issued, which leaves gaps between kernels, so that pass yields kernel durations,
-    # not `value`.  The persistent kernel's durations come from the timed launch itself.
-    roofline = None
-    n_local = kern.n
-    if live:
-        n_t = a.steps
-        frac = stored_fraction(burnin, thin, a.warmup + 1, a.warmup + a.steps)
-    else:
-        n_t = min(a.steps, a.timing_steps)
-        frac = stored_fraction(burnin, thin, a.warmup + a.steps + 1, a.warmup + a.steps + n_t)
-    bpu = algorithmic_bytes(D, K, frac, sink)
-    if timing:
-        if live:
-            kt = kt_live
-        else:
-            kern.set_timing(True)
-            run(n_t)
-            sync()
-            kt = kern.kernel_time()
-            kern.set_timing(False)
-        if kt["sweep_launches"]:
-            # kt["sweep_launches"] counts sweeps; the persistent kernel runs all n_t in ONE launch
-            t_sweep = kt["sweep_ms"] / kt["sweep_launches"] * 1e-3
-            spl = n_t if one_launch else 1               # sweeps per launch
-            t_launch = t_sweep * spl
-            units = chains * n_local * spl               # (chain, customer) sweeps per launch
-            achieved = bpu * units / t_launch / 1e9
-            kname = "persist_kernel" if persistent else "sweep_kernel"
-            roofline = dict(bound=None, achieved=round(achieved, 3), peak=HBM_PEAK_GBS, unit="GB/s",
-                            frac=round(achieved / HBM_PEAK_GBS, 6), traffic=None,
-                            kernel=("persist_kernel (one launch for all sweeps of a clv_run; level-2 workgroup "
-                                    "per chain" + ("; unit partials exchanged over xGMI" if p2p else "") + ")")
-                            if persistent else
-                            ("sweep_kernel (incl. fused level-2 tail)" if not sharded else "sweep_kernel"),
-                            bytes_per_unit=round(bpu, 3), units_per_launch=units, sweeps_per_launch=spl,
-                            launch_us=round(t_launch * 1e6, 3), sweep_kernel_us=round(t_sweep * 1e6, 3),
-                            timed_launches=kt["sweep_launches"] // spl,
-                            events=("the timed region's launch" if live else
-                                    f"a roofline pass of {n_t} further sweeps, one event pair per launch"))
-            tr = committed_traffic(a.workload, sharded and not p2p, kname, D, K)
-            if tr:  # HBM bytes per launch (calibrated PMC), per sweep x sweeps per launch
-                roofline["traffic"] = round(tr["bytes_per_sweep"] * spl)
-                roofline["traffic_source"] = f"{tr['source']}: {tr['counters']}"
-            if kt["hyper_launches"]:
-                roofline["hyper_kernel_us"] = round(kt["hyper_ms"] / kt["hyper_launches"] * 1e3, 3)
-            # bound: from the counters (HBM traffic rate vs peak, VALU busy share), not assumed
-            ev = committed_counters(a.workload, sharded and not p2p, kname, D, K) or {}
-            if roofline["traffic"] is not None:
-                ev["hbm_traffic_frac"] = round(roofline["traffic"] / t_launch / 1e9 / HBM_PEAK_GBS, 4)
-            if ev.get("hbm_traffic_frac", 0.0) >= 0.6:
-                roofline["bound"] = "hbm"
-            elif ev.get("valu_busy_frac", 0.0) >= 0.7:
-                roofline["bound"] = "valu"
-            elif "valu_busy_frac" in ev:
-                roofline["bound"] = "latency"
-            else:
-                roofline["bound"] = "unmeasured"
-            ev["rule"] = "hbm if measured HBM traffic >= 0.6 of peak; else valu if VALU busy >= 0.7; else latency"
-            roofline["bound_evidence"] = ev
-
-    kern.close()
+    legs = config_legs(world, name) if a.scaling_configs is None else [c for c in a.scaling_configs.split(",") if c]
     extra = {}
-    for name in [c for c in a.scaling_configs.split(",") if c]:
-        # warm-up of 200 sweeps (the launch-per-sweep path captures its 64-sweep hipGraph on first use;
-        # clocks ramp), then 1,000 timed sweeps: c4 ~0.09 s, c5 ~0.13 s per GPU
-        extra[name] = measure_config(name, world, rank, local_rank, dist, a.scaling_steps, 200, a.graph_chunk,
-                                     a.exchange if world > 1 else "rccl", settle_ms=a.clock_settle_ms)
-
-    if world == 1 and not a.force_sharded and a.c1_leg:
+    for leg in legs:
+        if leg == name:
+            continue
+        # c3 / c4 / c5 (and c2 tiled at N > 1): 200 warm-up sweeps (the launch-per-sweep path captures
+        # its hipGraph on first use; clocks ramp), then 1,000 timed sweeps per phase
+        extra[leg] = run_leg(leg, world, rank, local_rank, dist, a.scaling_steps, 200, graph_chunk=a.graph_chunk,
+                             exchange=exch, settle_ms=a.clock_settle_ms, stored_phase=a.stored_phase,
+                             timing_steps=a.timing_steps)
+        if world > 1 and leg == "c2":
+            extra[leg]["note"] = ("NOT a BASELINE configuration: c2's 23,570 CDNOW customers tiled once per rank "
+                                  "(a rehearsal of the CDNOW-size exchange at N GPUs)")
+        if world == 1 and a.whole_run and leg == "c3":
+            extra[leg]["whole_run"] = whole_run_e2e("c3")
+    if world == 1 and not a.force_sharded and a.c1_leg and "c1" not in (name,) and a.scaling_configs is None:
         # BASELINE configs[0] ("Bivariate M1, Abe 1/10 CDNOW subset, 4000 iters on CPU numpy reference
         # path"): the same 4-chain c1 sampler on the GPU (2,000 sweeps after 80), next to its 1-core
         # CPU leg in cpu_baseline["c1"]
-        extra["c1"] = measure_config("c1", 1, rank, local_rank, None, 2000, 80, 0, "rccl", stored_phase=False,
-                                     settle_ms=a.clock_settle_ms)
+        extra["c1"] = run_leg("c1", 1, rank, local_rank, None, 2000, 80, settle_ms=a.clock_settle_ms,
+                              stored_phase=False)
 
     if rank == 0:
         cpu = None
         if world == 1 and not a.no_cpu_baseline and not a.force_sharded:
-            cpu = cpu_baseline(a.workload)
-            if a.c1_leg and a.workload != "c1":
-                c1 = cpu_baseline("c1", parallel=False)
-                cpu["c1"] = dict(value=c1["value"], unit=c1["unit"], cores=1, kind=c1["kind"],
-                                 s_per_sweep=c1["s_per_sweep"], sample=c1["sample"],
-                                 gpu_value=extra["c1"]["value"] if "c1" in extra else None,
-                                 gpu_speedup=(extra["c1"]["value"] / c1["value"]) if "c1" in extra else None)
-        wl = WORKLOADS[a.workload]
+            cpu = cpu_baseline(name)
+            for leg in ("c1", "c3"):
+                if leg in extra and leg != name:
+                    c = cpu_baseline(leg, parallel=False)
+                    c.update(gpu_value=extra[leg]["value"], gpu_speedup=extra[leg]["value"] / c["value"])
+                    cpu[leg] = c
+                    extra[leg]["cpu_baseline"] = dict(value=c["value"], unit=c["unit"], cores=1, kind=c["kind"],
+                                                      s_per_sweep=c["s_per_sweep"], sample=c["sample"],
+                                                      gpu_speedup=c["gpu_speedup"])
+        for v in extra.values():
+            for k in ("_persistent", "_p2p", "_timed_region"):
+                v.pop(k, None)
+        n_total = prim["n_customers"]
         line = dict(
-            metric="MCMC sweeps/sec x N_customers (customer-sweeps/s)", value=value, unit="customer-sweeps/s",
-            n_gpus=world, steps=a.steps, warmup=a.warmup, ms_per_step=dt / a.steps * 1e3, higher_is_better=True,
+            metric="MCMC sweeps/sec x N_customers (customer-sweeps/s)", value=prim["value"], unit="customer-sweeps/s",
+            n_gpus=world, steps=a.steps, warmup=a.warmup, ms_per_step=prim["ms_per_step"], higher_is_better=True,
             scaling="weak", vs_baseline=None, dtype="f64",
             proposal_dtype="f32",  # t3 proposal noise and accept log-uniforms; state, posterior f64
-            data=(f"synthetic CBS ({n_total} customers, mcmc_clv_model_amd.data.synthetic_cbs)"
-                  if WORKLOADS[a.workload][1].startswith("synthetic:") else
-                  (f"CDNOW {WORKLOADS[a.workload][1]} CBS ({n_total // world:,} real customers, "
-                   f"tests/golden/cdnow_{WORKLOADS[a.workload][1]}_cbs.npz)")
+            ms_per_step_kind=("steady state: the GPU's clocks settled by clock_settle_ms of unrelated work before the "
+                              "warm-up; the timed call leaves its last level-2 draw pending (drawn at the start of the "
+                              "next call) — `cold` times the same steps from an idle GPU with that draw included")
+            if prim.get("_persistent") and not sharded else "wall time of the timed steps",
+            data=(f"synthetic CBS ({n_total} customers, mcmc_clv_model_amd.data.synthetic_cbs" +
+                  (f", {n_total // world:,} per GPU)" if world > 1 else ")")
+                  if data.startswith("synthetic:") else
+                  f"CDNOW {data} CBS ({n_total // world:,} real customers, tests/golden/cdnow_{data}_cbs.npz)"
                   + ("" if world == 1 else f", tiled x{world} (one copy per rank)")),
-            config=dict(workload=f"{a.workload}: {'bivariate' if D == 2 else 'trivariate'} M2, covariates {covs}",
-                        n_customers=n_total, chains=chains, n_mh_steps=20, burnin=burnin, mcmc=mcmc_workload,
+            config=dict(workload=f"{name}: {'bivariate' if D == 2 else 'trivariate'} M2, covariates {covs}",
+                        baseline_config=BASELINE_INDEX[name],
+                        n_customers=n_total, chains=chains, n_mh_steps=20, burnin=burnin, mcmc=mcmc,
                         thin=thin, seed=42, draw_sink=sink, parallelism=f"customer-shard x{world}",
                         **({"phase": "stored (profiling: burn-in 0, every sweep stores)"} if a.phase == "stored" else {}),
-                        timed_region=(f"one persistent-kernel launch of {a.steps} sweeps" if persistent else
-                                      "hipGraph replay of fused sweep launches") if not sharded else
-                        (f"one persistent-kernel launch of {a.steps} sweeps per rank, unit partials stored into "
-                         "every rank's IPC-mapped mail over xGMI (no host collective per sweep)") if p2p else
-                        f"torch.cuda graph replay ({a.graph_chunk} sweeps: sweep + group kernels, RCCL all_gather, "
-                        "level-2 kernel)" if a.graph_chunk else "eager: sweep + group kernels, RCCL all_gather, level-2"),
-            clock_settle_ms=round(settle_s * 1e3, 1),  # GPU busy with unrelated work before the warm-up
-            roofline=roofline, cpu_baseline=cpu,
-            host_us=(dict(host_us, clv_run_total=round(sum(host_us.values()), 3), timed_region=round(dt * 1e6, 3))
-                     if host_us else None),
-            exchange=(None if world == 1 and not sharded else
-                      dict(kind=kern.exchange, note=kern.p2p_note, requested=a.exchange if world > 1 else "rccl")),
-            speedup_vs_cpu_1core=(value / cpu["value"]) if cpu else None,
+                        timed_region=prim["_timed_region"]),
+            clock_settle_ms=prim["clock_settle_ms"],
+            roofline=prim["roofline"], cpu_baseline=cpu,
+            host_us=prim.get("host_us"),
+            cold=prim.get("cold"),
+            stored=prim.get("stored"),
+            whole_run=prim.get("whole_run"),
+            exchange=prim.get("exchange"),
+            path=prim["path"],
+            speedup_vs_cpu_1core=(prim["value"] / cpu["value"]) if cpu else None,
             configs=extra or None,
         )
         print(json.dumps(line))

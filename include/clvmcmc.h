@@ -207,6 +207,16 @@ int clv_note_sweeps(clv_sampler* s, int64_t n);
  * loglik: [chain][draw] per-draw mean of the likelihood term — bi:423-428.
  * Any pointer may be NULL. level1 requires draw_sink == CLV_SINK_FULL. */
 int clv_read_draws(clv_sampler* s, double* level1, double* level2, double* loglik);
+/* Stream the level-1 draws into the caller's host buffer while the sampler runs (world_size 1,
+ * CLV_SINK_FULL) — the drop-in's end-to-end time, run_mcmc_abe.py:60-77 around bi:437-504, instead
+ * of one pageable copy of every stored draw after the run.  level1: [chain][n_draws][n][D+2]
+ * doubles, caller-owned, valid until clv_read_draws with the same pointer (or NULL here, or
+ * clv_destroy).  Host threads of a process-wide copy pool first touch its pages, then each clv_run
+ * (its stored sweeps in sub-runs of >= 256 sweeps and ~64 MB of draws) hands the draws it completed
+ * to the pool (pinned staging, DMA on streams of the pool's own) and goes on sampling;
+ * clv_read_draws(s, level1, ...) waits for the copies in flight and copies what is left.  Same
+ * launches, same sweeps, same bits.  NULL stops streaming (after the copies in flight). */
+int clv_stream_draws(clv_sampler* s, double* level1);
 /* [chain][CLV_N_SUM_STATS][n] running sums over stored draws, and the number of stored draws. */
 int clv_read_summary(clv_sampler* s, double* sums, int64_t* n_stored);
 
@@ -229,10 +239,16 @@ int clv_kernel_time(clv_sampler* s, double* sweep_kernel_ms_total, int64_t* swee
 int clv_debug_host_times(const clv_sampler* s, int64_t* out);
 /* Philox4x32-10 on device: ctr/out are n x 4 words. */
 int clv_debug_philox(uint32_t k0, uint32_t k1, const uint32_t* ctr, int64_t n, uint32_t* out);
-/* The Philox-mode variates of one sweep for customers [0, n): t_l/t_m/u_acc are S x n. */
+/* The Philox-mode variates of one sweep for customers [0, n): t_l/t_m/u_acc are S x n;
+ * log2_u_acc (S x n, may be NULL) is the accept threshold's log2 U exactly as the sweep kernels
+ * form it (v_log_f32 of the fp32 uniform; bi:329-330 compares exp(lp' - lp) with U). */
 int clv_debug_variates(uint64_t seed, int32_t chain, uint32_t sweep, int64_t n, int32_t n_steps,
                        float* t_l, float* t_m, float* u_acc, double* u_z, double* u_tau,
-                       double* e_alive, double* eta_z);
+                       double* e_alive, double* eta_z, float* log2_u_acc);
+/* The accept threshold's log2 U over the Philox words [w_begin, w_end) (<= 2^32), against float64
+ * log2 of the same fp32 uniform: out[4] = max error in fp32 ulps of the exact value, max absolute
+ * error, the word with the largest ulp error, max ulp error where U <= 1/2. */
+int clv_debug_log2u_scan(uint64_t w_begin, uint64_t w_end, double* out);
 /* The MH proposal's Student-t(3) transforms on caller words (n x 3 uint32: radius word of t_l,
  * radius word of t_m, angle word: t_l takes its high 16 bits, t_m its low 16 bits), as the sweep
  * kernels form them (packed 0: t3_f32, 1: the trivariate launch-per-sweep kernels' t3_pair).

@@ -104,6 +104,7 @@ def lib() -> ctypes.CDLL:
         "clv_set_stream": (c_int32, [sp, c_uint64]),
         "clv_note_sweeps": (c_int32, [sp, c_int64]),
         "clv_read_draws": (c_int32, [sp, dp, dp, dp]),
+        "clv_stream_draws": (c_int32, [sp, dp]),
         "clv_read_summary": (c_int32, [sp, dp, POINTER(c_int64)]),
         "clv_get_state": (c_int32, [sp, dp, dp, dp]),
         "clv_set_state": (c_int32, [sp, dp, dp, dp, c_int64]),
@@ -111,7 +112,8 @@ def lib() -> ctypes.CDLL:
         "clv_kernel_time": (c_int32, [sp, dp, POINTER(c_int64), dp, POINTER(c_int64)]),
         "clv_debug_philox": (c_int32, [c_uint32, c_uint32, POINTER(c_uint32), c_int64, POINTER(c_uint32)]),
         "clv_debug_variates": (c_int32, [c_uint64, c_int32, c_uint32, c_int64, c_int32, POINTER(c_float),
-                                         POINTER(c_float), POINTER(c_float), dp, dp, dp, dp]),
+                                         POINTER(c_float), POINTER(c_float), dp, dp, dp, dp, POINTER(c_float)]),
+        "clv_debug_log2u_scan": (c_int32, [c_uint64, c_uint64, dp]),
         "clv_debug_host_times": (c_int32, [sp, POINTER(c_int64)]),
         "clv_debug_t3": (c_int32, [POINTER(c_uint32), c_int64, c_int32, POINTER(c_float), POINTER(c_float)]),
         "clv_debug_level2": (c_int32, [c_int32, c_int32, POINTER(ClvPrior), dp, dp, dp, dp, dp, dp, dp]),

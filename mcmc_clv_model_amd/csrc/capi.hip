@@ -78,7 +78,7 @@ SweepArgs sweep_args(clv_sampler* s, int init, int fuse = 0) {
   a.hyper_out = s->d_hyper_alt ? s->d_hyper_alt : s->d_hyper;
   a.wait_ticks = s->wait_ticks;
   a.abort_host = s->d_h_abort;
-  a.pre_variates = s->pre_variates;
+  a.diag = s->d_diag;
   a.h = hyper_args(s, nullptr, 0);
   if (fuse) a.h.hvar = s->replay ? nullptr : s->d_hvar;
   return a;
@@ -192,6 +192,83 @@ int build_graph(clv_sampler* s, int n) {
 }
 
 bool is_pow2(int v) { return v > 0 && (v & (v - 1)) == 0; }
+
+// Draws stored by the first `sweeps` sweeps (per chain): bi:402's condition, capped at n_draws.
+int64_t stored_count(const clv_sampler* s, int64_t sweeps) {
+  const Geometry& g = s->g;
+  if (sweeps <= g.burnin || g.n_draws <= 0) return 0;
+  return std::min<int64_t>((sweeps - 1 - g.burnin) / g.thin + 1, g.n_draws);
+}
+
+// Hand the level-1 draws completed since the last call to the copy pool (clv_stream_draws).
+void stream_enqueue(clv_sampler* s) {
+  if (!s->ds_dest || !s->d_level1) return;
+  const Geometry& g = s->g;
+  const int64_t k = stored_count(s, s->sweeps_done);
+  if (k <= s->ds_next) return;
+  const int64_t row = g.n * (g.D + 2);  // doubles per draw and chain
+  for (int c = 0; c < g.n_chains; ++c) {
+    const int64_t off = ((int64_t)c * g.n_draws + s->ds_next) * row;
+    stream_copy(s->ds, s->device, s->d_level1 + off, s->ds_dest + off, sizeof(double) * (size_t)((k - s->ds_next) * row));
+  }
+  s->ds_next = k;
+}
+
+// Before the draws already streamed may be rewritten (the state is set back): wait for the copies in
+// flight and stream again from the first draw the new sweep count has not stored.
+void stream_rewind(clv_sampler* s) {
+  if (!s->ds_dest) return;
+  stream_wait(s->ds);
+  s->ds_next = std::min(s->ds_next, stored_count(s, s->sweeps_done));
+}
+
+// The wait-timeout record of the last failed launch (kernels.hip report_wait) as text, and cleared
+// for the next one; "" if no wave recorded one.
+std::string take_wait_diag(clv_sampler* s) {
+  if (!s->d_diag) return "";
+  unsigned long long d[DIAG_WORDS] = {};
+  if (hipMemcpy(d, s->d_diag, sizeof(d), hipMemcpyDeviceToHost) != hipSuccess) return "";
+  (void)hipMemset(s->d_diag, 0, sizeof(d));
+  if (!d[0]) return "";
+  const Geometry& g = s->g;
+  const char* what = d[1] == WAIT_HYPER ? "(beta, Sigma) hand-off slot"
+                     : d[1] == WAIT_BLOCKS ? "block partial"
+                     : d[1] == WAIT_P2P_MAIL ? "peer unit partial (persistent)" : "peer unit partial (fused)";
+  std::string m = std::string(" [wait record: sweep ") + std::to_string((long long)d[2]) + ", chain " +
+                  std::to_string(d[3]) + ", rank " + std::to_string(d[4]) + ": " + what + " ";
+  const long long unit = (long long)d[5];
+  if ((d[1] == WAIT_P2P_MAIL || d[1] == WAIT_FX_MAIL) && g.units_per_rank > 0 && unit >= 0)
+    m += "unit " + std::to_string(unit) + " (rank " + std::to_string(unit / g.units_per_rank) + ", local unit " +
+         std::to_string(unit % g.units_per_rank) + ")";
+  else
+    m += (d[1] == WAIT_HYPER ? "of block " : "") + std::to_string(unit);
+  char bits[32];
+  std::snprintf(bits, sizeof(bits), "%016llx", d[7]);
+  m += " statistic " + std::to_string((long long)d[6]) + " still empty (bits " + bits + ") after " +
+       std::to_string(d[8]) + " polls, " + std::to_string(d[9] / 100000.0) + " ms; " + std::to_string(d[10]) +
+       " lanes of the wave missing";
+  if (d[1] == WAIT_P2P_MAIL || d[1] == WAIT_FX_MAIL) {
+    m += "; progress (sweep each rank's level-2 side last polled for):";
+    for (int q = 0; q < std::min(g.world_size, 5); ++q)
+      m += " " + std::to_string(q) + ":" + (d[11 + q] == ~0ull ? std::string("none") : std::to_string((long long)d[11 + q]));
+  }
+  return m + "]";
+}
+
+// CLV_WAIT_TIMEOUT_MS: a finite decimal number (surrounding blanks allowed; no hex, inf or nan),
+// clamped to the range clv_set_wait_timeout accepts, [1 ms, 1 h].  distributed.run_wait_ms applies
+// the same rule in Python.
+bool parse_wait_ms(const char* txt, double* ms) {
+  for (const char* c = txt; *c; ++c)
+    if (*c == 'x' || *c == 'X' || *c == 'n' || *c == 'N' || *c == 'i' || *c == 'I') return false;
+  char* end = nullptr;
+  const double v = std::strtod(txt, &end);
+  if (end == txt) return false;
+  while (*end == ' ' || *end == '\t' || *end == '\n') ++end;
+  if (*end || !(v == v) || v > 1e300 || v < -1e300) return false;
+  *ms = std::min(3.6e6, std::max(1.0, v));
+  return true;
+}
 
 }  // namespace
 
@@ -480,7 +557,8 @@ int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* pri
   if (!s->replay && cfg->world_size > 1 && cfg->world_size <= MAX_WORLD && g.n_units_global <= 2 * BLOCK)
     s->fx_capable = true;
   if (s->p2p_capable || s->fx_capable) {
-    const int64_t nm = 2LL * g.world_size * C * g.stride * g.units_per_rank;
+    // the slots, then one progress word per rank (MAIL_TAIL)
+    const int64_t nm = mail_slots(g.world_size, (int)C, g.stride, g.units_per_rank) + MAIL_TAIL;
     // The mail is written by OTHER GPUs (system-scope write-through stores over xGMI) while this
     // GPU polls it.  Uncached device memory (MTYPE UC: every access of every agent goes to memory,
     // no L2 line of this GPU can hold a stale copy of a peer's store); fine-grained, then plain
@@ -516,31 +594,25 @@ int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* pri
     CLV_HIPC(dalloc(&s->d_hyper_alt, C * HS));
     if ((cfg->draw_sink == CLV_SINK_SUMMARY || cfg->draw_sink == CLV_SINK_SUMMARY_PCT) && n > 0)
       CLV_HIPC(dalloc(&s->d_sums_prev, (size_t)C * CLV_N_SUM_STATS * n));
+    CLV_HIPC(dalloc(&s->d_diag, DIAG_WORDS));
+    CLV_HIPC(hipMemsetAsync(s->d_diag, 0, sizeof(unsigned long long) * DIAG_WORDS, s->stream));
     CLV_HIPC(hipHostMalloc((void**)&s->h_abort, sizeof(uint32_t), hipHostMallocMapped));
     *s->h_abort = 0;
     CLV_HIPC(hipHostGetDevicePointer((void**)&s->d_h_abort, s->h_abort, 0));
     // every wait of the persistent kernel is bounded: 2 s at world size 1 (all workgroups are
     // resident, so a wait that long means a fault), 10 s with peers (host-side launch skew between
     // ranks); CLV_WAIT_TIMEOUT_MS overrides
-    const char* env = std::getenv("CLV_WAIT_TIMEOUT_MS");
-    const double ms = env ? std::atof(env) : (cfg->world_size > 1 ? 10000.0 : 2000.0);
-    s->wait_ticks = (uint64_t)(std::max(1.0, ms) * 1e5);  // s_memrealtime: 100 MHz
+    double ms = cfg->world_size > 1 ? 10000.0 : 2000.0;
+    if (const char* env = std::getenv("CLV_WAIT_TIMEOUT_MS")) {
+      if (!parse_wait_ms(env, &ms))
+        return cleanup_fail(fail(CLV_EINVAL, "CLV_WAIT_TIMEOUT_MS must be a finite decimal number of ms"));
+    }
+    s->wait_ticks = (uint64_t)(ms * 1e5);  // s_memrealtime: 100 MHz
   }
-  {
-    const char* env = std::getenv("CLV_SYNC");
-    if (env) s->sync_mode = std::max(0, std::min(2, std::atoi(env)));
-    env = std::getenv("CLV_TIMING_RECORD");
-    s->timing_record = !(env && std::string(env) == "0");
-    env = std::getenv("CLV_PRE_VARIATES");  // 0: MH variates drawn inside the MH phase (A/B)
-    s->pre_variates = (env && std::string(env) == "0") ? 0 : 1;
-  }
-  if ((s->persistent || s->p2p_capable) && s->n_cu > 0) {
-    // default on for the bivariate model only: measured c2 13.44 -> 12.94 us per sweep, but c3
-    // (trivariate: longer level-2 draw, so both waves of a same-chain pair idle in the hand-off
-    // together) 16.36 -> 17.31.  CLV_WG_MAP=1 forces it, =0 disables it.
-    const char* env = std::getenv("CLV_WG_MAP");
-    const bool on = env ? std::string(env) != "0" : g.D == 2;
-    if (on) {
+  if ((s->persistent || s->p2p_capable) && s->n_cu > 0 && g.D == 2) {
+    // the bivariate model only: measured c2 13.44 -> 12.94 us per sweep, but c3 (trivariate: longer
+    // level-2 draw, so both waves of a same-chain pair idle in the hand-off together) 16.36 -> 17.31
+    {
       std::vector<int32_t> map = persist_wg_map((int)C, (int)nb_local, s->n_cu);
       CLV_HIPC(dalloc(&s->d_wgmap, map.size()));
       CLV_HIPC(hipMemcpy(s->d_wgmap, map.data(), sizeof(int32_t) * map.size(), hipMemcpyHostToDevice));
@@ -641,6 +713,10 @@ void clv_destroy(clv_sampler* s) {
   if (!s) return;
   (void)hipSetDevice(s->device);
   if (s->stream) (void)hipStreamSynchronize(s->stream);
+  if (s->ds) {  // no copy may still read the draws freed below
+    stream_wait(s->ds);
+    delete s->ds;
+  }
   if (s->graph_exec) (void)hipGraphExecDestroy(s->graph_exec);
   for (auto e : s->ev) (void)hipEventDestroy(e);
   if (s->done_ev) (void)hipEventDestroy(s->done_ev);
@@ -652,7 +728,7 @@ void clv_destroy(clv_sampler* s) {
   if (s->d_unit && s->d_unit != s->d_block) (void)hipFree(s->d_unit);
   if (s->d_hyp2) (void)hipFree(s->d_hyp2);
   for (void* p : {(void*)s->d_lam_alt, (void*)s->d_mu_alt, (void*)s->d_hyper_alt, (void*)s->d_sums_prev,
-                  (void*)s->d_pblock, (void*)s->d_qstore, (void*)s->d_pend})
+                  (void*)s->d_pblock, (void*)s->d_qstore, (void*)s->d_pend, (void*)s->d_diag})
     if (p) (void)hipFree(p);
   if (s->h_abort) (void)hipHostFree(s->h_abort);
   for (void* p : s->ipc_opened) (void)hipIpcCloseMemHandle(p);
@@ -793,7 +869,7 @@ int clv_p2p_connect(clv_sampler* s, const void* handles, const uint64_t* ptrs) {
   }
   {  // every slot of this rank's mail empty (a failed step may have left units of any rank there);
      // the caller synchronises the ranks after connecting, before any rank runs
-    const int64_t nm = 2LL * s->g.world_size * s->g.n_chains * s->g.stride * s->g.units_per_rank;
+    const int64_t nm = mail_slots(s->g.world_size, s->g.n_chains, s->g.stride, s->g.units_per_rank) + MAIL_TAIL;
     CLV_HIP(hipMemsetAsync(s->d_mail, 0xFF, sizeof(double) * nm, s->stream));
   }
   const int W = s->g.world_size, r = s->cfg.rank;
@@ -894,28 +970,21 @@ int clv::persist_launch(clv_sampler* s, int64_t n_sweeps) {
     if (s->ev_sweeps.size() < TIMING_EVENTS) s->ev_sweeps.assign(TIMING_EVENTS, 1);
     s->ev_sweeps[s->ev_used] = n_sweeps;
   }
-  if (s->timing_record && e0) {  // events recorded around the launch: measured 0.4-0.7 us per step
-                                 // less host cost on the driver's 20-sweep run than the dispatch's
-                                 // own timestamps (hipExtLaunchKernelGGL), same duration to 0.2%
-    CLV_HIP(hipEventRecord(e0, s->stream));
-    s->host_ns[2] = host_now_ns();
-    CLV_HIP(launch_persist(a, s->sweeps_done + 1, n_sweeps, s->stream, nullptr, nullptr));
-    s->host_ns[3] = host_now_ns();
-    CLV_HIP(hipEventRecord(e1, s->stream));
-  } else {
-    s->host_ns[2] = host_now_ns();
-    CLV_HIP(launch_persist(a, s->sweeps_done + 1, n_sweeps, s->stream, e0, e1));
-    s->host_ns[3] = host_now_ns();
-  }
-  // the launch's end event (timing: the dispatch's own end timestamp; else one recorded behind
-  // it).  Timed launches are harvested later (clv_kernel_time or a full slot set).
+  // timed launches: events recorded around the launch (measured 0.4-0.7 us per step less host cost
+  // on the driver's 20-sweep run than the dispatch's own timestamps, same duration to 0.2%)
+  if (e0) CLV_HIP(hipEventRecord(e0, s->stream));
+  s->host_ns[2] = host_now_ns();
+  CLV_HIP(launch_persist(a, s->sweeps_done + 1, n_sweeps, s->stream, nullptr, nullptr));
+  s->host_ns[3] = host_now_ns();
+  if (e1) CLV_HIP(hipEventRecord(e1, s->stream));
+  // the launch's end event; timed launches are harvested later (clv_kernel_time or a full slot set)
   s->inflight_done = e1;
   if (s->timing) {
     if (++s->ev_used == TIMING_EVENTS) {
       int rc = harvest_timing(s);
       if (rc) return rc;
     }
-  } else if (s->sync_mode != 0) {
+  } else {
     if (!s->done_ev) CLV_HIP(hipEventCreateWithFlags(&s->done_ev, hipEventDisableTiming));
     CLV_HIP(hipEventRecord(s->done_ev, s->stream));
     s->inflight_done = s->done_ev;
@@ -930,16 +999,16 @@ int clv::persist_wait(clv_sampler* s) {
   if (n_sweeps == 0) return CLV_OK;
   s->inflight_n = 0;
   const Geometry& g = s->g;
+  // the host polls the launch's end event (stream synchronize / event synchronize measured within
+  // 0.3 us per step of it, profiles/r04_host_variants.jsonl)
   const hipEvent_t done = s->inflight_done;
-  if (s->sync_mode == 0 || !done) {
+  if (!done) {
     CLV_HIP(hipStreamSynchronize(s->stream));
-  } else if (s->sync_mode == 1) {
+  } else {
     hipError_t q;
     while ((q = hipEventQuery(done)) == hipErrorNotReady) {
     }
     CLV_HIP(q);
-  } else {
-    CLV_HIP(hipEventSynchronize(done));
   }
   s->host_ns[5] = host_now_ns();
   if (__atomic_load_n(s->h_abort, __ATOMIC_ACQUIRE)) {
@@ -953,11 +1022,12 @@ int clv::persist_wait(clv_sampler* s) {
     if (s->d_sums_prev) CLV_HIP(hipMemcpy(s->d_sums, s->d_sums_prev, sums_bytes, hipMemcpyDeviceToDevice));
     s->slots_dirty = true;
     if (g.world_size > 1) s->p2p_ready = false;  // mail slots are in an unknown state now
-    return fail(CLV_EHIP, g.world_size > 1
-                              ? "persistent sweep kernel: a wait timed out (a peer rank not running, or not all resident?); "
-                                "state unchanged"
-                              : "persistent sweep kernel: a workgroup timed out waiting for its chain (not all resident?); "
-                                "state unchanged");
+    const std::string diag = take_wait_diag(s);
+    return fail(CLV_EHIP, std::string(g.world_size > 1
+                                          ? "persistent sweep kernel: a wait timed out (a peer rank not running, or not all "
+                                            "resident?); state unchanged"
+                                          : "persistent sweep kernel: a workgroup timed out waiting for its chain (not all "
+                                            "resident?); state unchanged") + diag);
   }
   std::swap(s->d_lam, s->d_lam_alt);
   std::swap(s->d_mu, s->d_mu_alt);
@@ -1089,7 +1159,33 @@ int run_fused_exchange(clv_sampler* s, int64_t n_sweeps) {
   CLV_HIP(hipMemset(s->d_arrive, 0, sizeof(uint32_t) * (g.n_chains + (int64_t)g.n_chains * g.units_per_rank)));
   s->p2p_ready = false;  // mail slots in an unknown state: clv_p2p_connect refills them
   if (rc) return rc;
-  return fail(CLV_EHIP, "fused peer exchange: a wait timed out (a peer rank not running?); state unchanged");
+  return fail(CLV_EHIP, "fused peer exchange: a wait timed out (a peer rank not running?); state unchanged" +
+                            take_wait_diag(s));
+}
+
+// World size 1 with the draws streamed to the host (clv_stream_draws): the burn-in in one go, the
+// stored sweeps in sub-runs of >= 256 sweeps and ~64 MB of draws, each sub-run's draws handed to the
+// copy pool while the next one runs (the same launches' sweeps in the same order: the same bits).
+int run_streaming(clv_sampler* s, int64_t n_sweeps) {
+  const Geometry& g = s->g;
+  const int64_t per_draw = (int64_t)g.n_chains * g.n * (g.D + 2) * (int64_t)sizeof(double);
+  const int64_t chunk = std::max<int64_t>(256, std::max<int64_t>(1, (64LL << 20) / std::max<int64_t>(per_draw, 1)) * g.thin);
+  int64_t left = n_sweeps;
+  while (left > 0) {
+    const int64_t k = s->sweeps_done < g.burnin ? std::min<int64_t>(left, g.burnin - s->sweeps_done)
+                                                : std::min<int64_t>(left, chunk);
+    int rc;
+    if (s->persistent) {
+      rc = run_persistent(s, k);
+    } else {
+      rc = enqueue_fused_sweeps(s, k);
+      if (rc == CLV_OK && hipStreamSynchronize(s->stream) != hipSuccess) rc = fail(CLV_EHIP, "hipStreamSynchronize");
+    }
+    if (rc) return rc;
+    stream_enqueue(s);
+    left -= k;
+  }
+  return CLV_OK;
 }
 }  // namespace
 
@@ -1116,6 +1212,7 @@ int clv_run(clv_sampler* s, int64_t n_sweeps) {
     if (rc) return rc;
     s->pending_init_hyper = false;
   }
+  if (s->ds_dest) return run_streaming(s, n_sweeps);
   if (s->persistent) {
     rc = run_persistent(s, n_sweeps);
     s->host_ns[6] = host_now_ns();
@@ -1127,8 +1224,28 @@ int clv_run(clv_sampler* s, int64_t n_sweeps) {
   return CLV_OK;
 }
 
+int clv_stream_draws(clv_sampler* s, double* level1) {
+  if (!s) return fail(CLV_EINVAL, "null sampler");
+  if (s->ds) stream_wait(s->ds);
+  if (!level1) {
+    s->ds_dest = nullptr;
+    return CLV_OK;
+  }
+  if (s->g.world_size != 1) return fail(CLV_ESTATE, "draw streaming needs world_size 1");
+  if (!s->d_level1) return fail(CLV_ESTATE, "draw streaming needs draw_sink == CLV_SINK_FULL with draws to store");
+  CLV_HIP(hipSetDevice(s->device));
+  if (!s->ds) s->ds = new DrawStreamState();
+  s->ds_dest = level1;
+  s->ds_next = 0;
+  const Geometry& g = s->g;
+  stream_prefault(s->ds, s->device, level1, sizeof(double) * (size_t)g.n_chains * g.n_draws * g.n * (g.D + 2));
+  stream_enqueue(s);  // draws of sweeps already run
+  return CLV_OK;
+}
+
 int clv_rollback(clv_sampler* s) {
   if (!s) return fail(CLV_EINVAL, "null sampler");
+  if (s->ds_dest) return fail(CLV_ESTATE, "clv_rollback while the draws are streamed (clv_stream_draws)");
   if (s->last_persist_n <= 0) return fail(CLV_ESTATE, "nothing to roll back (the last call was not a completed persistent clv_run)");
   CLV_HIP(hipSetDevice(s->device));
   CLV_HIP(hipStreamSynchronize(s->stream));
@@ -1167,7 +1284,20 @@ int clv_read_draws(clv_sampler* s, double* level1, double* level2, double* logli
   const size_t C = g.n_chains;
   if (level1) {
     if (!s->d_level1 && g.n_draws > 0 && g.n > 0) return fail(CLV_ESTATE, "level-1 draws need draw_sink == CLV_SINK_FULL");
-    if (s->d_level1)
+    bool done = false;
+    if (s->ds_dest == level1) {  // streamed: the rest of the stored draws, then wait for every copy
+      stream_enqueue(s);
+      done = stream_wait(s->ds);
+      // (draws beyond the stored ones are never written: zeros, as the device buffer holds)
+      const int64_t k = stored_count(s, s->sweeps_done);
+      if (done && k < g.n_draws)
+        for (size_t c = 0; c < C; ++c)
+          std::memset(level1 + ((int64_t)c * g.n_draws + k) * g.n * (g.D + 2), 0,
+                      sizeof(double) * (size_t)((g.n_draws - k) * g.n * (g.D + 2)));
+    } else if (s->ds) {
+      stream_wait(s->ds);
+    }
+    if (s->d_level1 && !done)
       CLV_HIP(hipMemcpy(level1, s->d_level1, sizeof(double) * C * g.n_draws * g.n * (g.D + 2), hipMemcpyDeviceToHost));
   }
   if (level2 && s->d_level2)
@@ -1246,6 +1376,7 @@ int clv_set_state(clv_sampler* s, const double* lambdas, const double* mus, cons
   CLV_HIP(hipStreamSynchronize(s->stream));
   s->sweeps_done = sweeps_done;
   s->last_persist_n = 0;
+  stream_rewind(s);
   return CLV_OK;
 }
 
@@ -1313,30 +1444,57 @@ int clv_debug_philox(uint32_t k0, uint32_t k1, const uint32_t* ctr, int64_t n, u
 }
 
 int clv_debug_variates(uint64_t seed, int32_t chain, uint32_t sweep, int64_t n, int32_t S, float* tl, float* tm,
-                       float* ua, double* uz, double* ut, double* ea, double* ez) {
+                       float* ua, double* uz, double* ut, double* ea, double* ez, float* l2u) {
   if (n < 1 || S < 0) return fail(CLV_EINVAL, "bad arguments");
   const int64_t nS = std::max<int64_t>(n * S, 1);
-  float *dtl, *dtm, *dua;
+  float *dtl, *dtm, *dua, *dl2u;
   double *duz, *dut, *dea, *dez;
   CLV_HIP(dalloc(&dtl, nS));
   CLV_HIP(dalloc(&dtm, nS));
   CLV_HIP(dalloc(&dua, nS));
+  CLV_HIP(dalloc(&dl2u, nS));
   CLV_HIP(dalloc(&duz, n));
   CLV_HIP(dalloc(&dut, n));
   CLV_HIP(dalloc(&dea, n));
   CLV_HIP(dalloc(&dez, n));
-  CLV_HIP(launch_debug_variates(seed, chain, sweep, n, S, dtl, dtm, dua, duz, dut, dea, dez, nullptr));
+  CLV_HIP(launch_debug_variates(seed, chain, sweep, n, S, dtl, dtm, dua, dl2u, duz, dut, dea, dez, nullptr));
   if (S > 0) {
     CLV_HIP(hipMemcpy(tl, dtl, sizeof(float) * n * S, hipMemcpyDeviceToHost));
     CLV_HIP(hipMemcpy(tm, dtm, sizeof(float) * n * S, hipMemcpyDeviceToHost));
     CLV_HIP(hipMemcpy(ua, dua, sizeof(float) * n * S, hipMemcpyDeviceToHost));
+    if (l2u) CLV_HIP(hipMemcpy(l2u, dl2u, sizeof(float) * n * S, hipMemcpyDeviceToHost));
   }
   CLV_HIP(hipMemcpy(uz, duz, sizeof(double) * n, hipMemcpyDeviceToHost));
   CLV_HIP(hipMemcpy(ut, dut, sizeof(double) * n, hipMemcpyDeviceToHost));
   CLV_HIP(hipMemcpy(ea, dea, sizeof(double) * n, hipMemcpyDeviceToHost));
   CLV_HIP(hipMemcpy(ez, dez, sizeof(double) * n, hipMemcpyDeviceToHost));
-  for (void* p : {(void*)dtl, (void*)dtm, (void*)dua, (void*)duz, (void*)dut, (void*)dea, (void*)dez})
+  for (void* p : {(void*)dtl, (void*)dtm, (void*)dua, (void*)dl2u, (void*)duz, (void*)dut, (void*)dea, (void*)dez})
     CLV_HIP(hipFree(p));
+  return CLV_OK;
+}
+
+int clv_debug_log2u_scan(uint64_t w_begin, uint64_t w_end, double* out) {
+  if (!out || w_end > (1ull << 32) || w_begin >= w_end) return fail(CLV_EINVAL, "bad arguments");
+  constexpr int NB = 4096;
+  double* dres = nullptr;
+  CLV_HIP(dalloc(&dres, 4 * NB));
+  CLV_HIP(launch_debug_log2u_scan(w_begin, w_end, NB, dres, nullptr));
+  std::vector<double> r(4 * NB);
+  CLV_HIP(hipMemcpy(r.data(), dres, sizeof(double) * r.size(), hipMemcpyDeviceToHost));
+  CLV_HIP(hipFree(dres));
+  double mu = 0.0, ma = 0.0, wu = 0.0, mu_far = 0.0;
+  for (int b = 0; b < NB; ++b) {
+    if (r[4 * b] > mu) {
+      mu = r[4 * b];
+      wu = r[4 * b + 2];
+    }
+    ma = std::max(ma, r[4 * b + 1]);
+    mu_far = std::max(mu_far, r[4 * b + 3]);
+  }
+  out[0] = mu;      // max error in fp32 ulps of the exact log2
+  out[1] = ma;      // max absolute error
+  out[2] = wu;      // the word where the ulp error is largest
+  out[3] = mu_far;  // max ulp error where U <= 1/2 (|log2 U| >= 1)
   return CLV_OK;
 }
 

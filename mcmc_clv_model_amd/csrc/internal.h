@@ -3,6 +3,9 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+#include <condition_variable>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -22,6 +25,18 @@ int persist_flush(clv_sampler* s);  // the deferred level-2 draw, if one is pend
 // admitting blocks_per_cu of its workgroups each (capi.hip).
 bool persist_grid_fits(int64_t grid_wgs, int blocks_per_cu, int n_cu);
 bool persist_worth(int D, int K, int n_chains, int64_t grid_wgs, int n_cu);
+
+// Level-1 draws streamed to a host buffer during the run (drawstream.hip): the pieces a sampler has
+// in flight in the process-wide copy pool, and whether any failed.
+struct DrawStreamState {
+  std::mutex m;
+  std::condition_variable cv;
+  int64_t pending = 0;
+  std::atomic<int> failed{0};
+};
+void stream_prefault(DrawStreamState* st, int device, void* dst, size_t bytes);  // touch dst's pages
+void stream_copy(DrawStreamState* st, int device, const void* src, void* dst, size_t bytes);
+bool stream_wait(DrawStreamState* st);  // every piece done; false if one failed (then reset)
 
 template <class T>
 hipError_t dalloc(T** p, size_t count) {
@@ -92,6 +107,7 @@ struct clv_sampler {
   double* d_sums_prev = nullptr;    // summary sink: the running sums before the last persistent launch
   uint32_t* h_abort = nullptr;      // host-mapped copy of ctrl->abort (the kernel stores it on a timeout)
   uint32_t* d_h_abort = nullptr;    // its device address
+  unsigned long long* d_diag = nullptr;  // wait-timeout record (kernels.hip report_wait), DIAG_WORDS
   uint64_t wait_ticks = 0;          // bound on every persistent-kernel wait (s_memrealtime ticks)
   bool slots_dirty = true;          // persistent hand-off slots need the sentinel fill (a completed
                                     // launch leaves them empty; only an aborted one does not)
@@ -134,19 +150,19 @@ struct clv_sampler {
   hipGraphExec_t graph_exec = nullptr;
   int graph_sweeps = 0;
 
-  // how clv_run waits for a persistent launch (CLV_SYNC, read at create): 0 hipStreamSynchronize,
-  // 1 poll hipEventQuery on the launch's end event, 2 hipEventSynchronize on it
-  int sync_mode = 1;
+  // clv_run waits for a persistent launch by polling its end event
   hipEvent_t done_ev = nullptr;     // recorded after each untimed persistent launch (timing: e1)
   int64_t inflight_n = 0;           // sweeps of the persistent launch in flight (persist_launch)
   hipEvent_t inflight_done = nullptr;  // its end event (null: wait with hipStreamSynchronize)
-  int pre_variates = 1;             // CLV_PRE_VARIATES (read at create)
-  bool timing_record = true;        // timed persistent launches bracketed by hipEventRecord
-                                    // (CLV_TIMING_RECORD=0: the dispatch's own timestamps)
 
   // host clock (steady_clock, ns) at the steps of the last persistent clv_run: entry, after
   // hipSetDevice, before the launch call, after it, after the end-event record, wait done, return
   int64_t host_ns[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+
+  // clv_stream_draws: the caller's level-1 buffer and the draws (per chain) handed to the copy pool
+  clv::DrawStreamState* ds = nullptr;
+  double* ds_dest = nullptr;
+  int64_t ds_next = 0;
 
   bool timing = false;
   std::vector<hipEvent_t> ev;  // 4 per slot: sweep start/end, hyper start/end

@@ -16,6 +16,15 @@ constexpr int UMAIL = 2048;            // persistent kernel, world size > 1: LDS
                                        // unit partials (stride * local units must fit)
 constexpr int HV = 40;                 // precomputed Philox hyper variates per chain: iw normals [0,3),
                                        // chi2 [3,6), beta normals [8,35)
+constexpr int MAIL_TAIL = MAX_WORLD;   // peer mail: after the [2][world][chain][unit][stat] slots, one
+                                       // progress word per rank (the sweep its level-2 side last polled for)
+constexpr int DIAG_WORDS = 16;         // wait-timeout record (SweepArgs::diag, see kernels.hip report_wait)
+enum : int { WAIT_HYPER = 1, WAIT_BLOCKS = 2, WAIT_P2P_MAIL = 3, WAIT_FX_MAIL = 4 };
+
+// Doubles of peer-mail slots before the progress words.
+__host__ __device__ inline int64_t mail_slots(int world, int chains, int stride, int units_per_rank) {
+  return 2LL * world * chains * stride * units_per_rank;
+}
 
 // Hyper-state layout (per chain, HS doubles).
 enum : int {
@@ -111,7 +120,6 @@ struct SweepArgs {
   double* const* peers;      // [world] device pointers to every rank's mail buffer (peers[rank] = mail)
   int rank;
   const int32_t* wg_map;     // persistent kernel: linear workgroup -> (chain << 16 | block), or null
-  int pre_variates;          // persistent kernel: draw the next sweep's MH variates during the hand-off
   // persistent kernel: the carried state at the end of a launch goes to these (the host swaps them
   // with lam / mu / hyper only if no wave aborted), the bound on every wait (s_memrealtime ticks,
   // 100 MHz) and a host-mapped copy of ctrl->abort (read by the host after the launch, no D2H copy)
@@ -127,6 +135,10 @@ struct SweepArgs {
   double* pend_out;
   uint64_t wait_ticks;
   uint32_t* abort_host;
+  // wait-timeout record (device memory, DIAG_WORDS, zero when none): the first wave whose bounded
+  // wait expires claims word 0 and writes what it was waiting for (kernels.hip report_wait); the
+  // host formats it into clv_last_error()
+  unsigned long long* diag;
   HyperArgs h;               // level-2 arguments of the fused tail
   unsigned long long* stamps; // diagnostic build only (CLV_STAMPS): [1024][8] s_memrealtime stamps
 };
@@ -153,8 +165,9 @@ hipError_t launch_set_hyper(int D, int K, int n_chains, double* hyper, const dou
 hipError_t launch_debug_philox(uint32_t k0, uint32_t k1, const uint32_t* ctr, int64_t n, uint32_t* out,
                                hipStream_t st);
 hipError_t launch_debug_variates(uint64_t seed, int chain, uint32_t sweep, int64_t n, int S, float* tl,
-                                 float* tm, float* ua, double* uz, double* ut, double* ea, double* ez,
+                                 float* tm, float* ua, float* l2u, double* uz, double* ut, double* ea, double* ez,
                                  hipStream_t st);
+hipError_t launch_debug_log2u_scan(uint64_t w_begin, uint64_t w_end, int n_blocks, double* out, hipStream_t st);
 hipError_t launch_debug_t3(const uint32_t* w, int64_t n, int packed, float* tl, float* tm, hipStream_t st);
 hipError_t launch_debug_level2(int D, int K, const double* prior_dev, const double* in, double* out,
                                hipStream_t st);

@@ -1078,6 +1078,51 @@ __device__ __forceinline__ bool wait_expired(const SweepArgs& a, uint64_t t0, ui
   return false;
 }
 
+// The wait-timeout record (SweepArgs::diag): the wave whose bounded wait expired names what it was
+// waiting for — the lowest lane still missing a slot reports its (unit or block, statistic, the
+// bits it read) — and, with peers, the progress words in this rank's mail (the sweep each rank's
+// level-2 side last started to poll for).  Word layout: [0] claimed, [1] kind (WAIT_*), [2] sweep,
+// [3] chain, [4] rank, [5] unit / block, [6] statistic, [7] bits, [8] polls, [9] waited ticks
+// (100 MHz), [10] lanes of the wave still missing, [11..15] progress of ranks 0..4 (-1: none).
+// Called by every lane of the wave (one ballot); only the first wave of the launch to time out writes.
+__device__ __forceinline__ void report_wait(const SweepArgs& a, int kind, int64_t s, int c, bool lane_ok,
+                                            int64_t unit, int stat, uint64_t bits, uint32_t polls, uint64_t t0) {
+  if (!a.diag) return;
+  const uint64_t miss = __ballot(!lane_ok);
+  if (!miss) return;
+  const int first = __ffsll((unsigned long long)miss) - 1;
+  if ((int)(threadIdx.x & 63) != first) return;
+  if (atomicCAS(a.diag, 0ull, 1ull) != 0ull) return;
+  a.diag[1] = (unsigned long long)kind;
+  a.diag[2] = (unsigned long long)s;
+  a.diag[3] = (unsigned long long)c;
+  a.diag[4] = (unsigned long long)a.rank;
+  a.diag[5] = (unsigned long long)unit;
+  a.diag[6] = (unsigned long long)stat;
+  a.diag[7] = bits;
+  a.diag[8] = polls;
+  a.diag[9] = __builtin_amdgcn_s_memrealtime() - t0;
+  a.diag[10] = (unsigned long long)__popcll(miss);
+  const Geometry& g = a.g;
+  for (int q = 0; q < 5; ++q) {
+    unsigned long long v = ~0ull;
+    if (a.mail && q < g.world_size)
+      v = __builtin_bit_cast(unsigned long long,
+                             __hip_atomic_load(a.mail + mail_slots(g.world_size, g.n_chains, g.stride, g.units_per_rank) + q,
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+    a.diag[11 + q] = v;
+  }
+}
+
+// This rank's level-2 side starts to poll for sweep s: its progress word in every rank's mail.
+__device__ __forceinline__ void post_progress(const SweepArgs& a, double* const* peers, int64_t s) {
+  const Geometry& g = a.g;
+  const int64_t off = mail_slots(g.world_size, g.n_chains, g.stride, g.units_per_rank) + a.rank;
+  for (int q = 0; q < g.world_size; ++q)
+    __hip_atomic_store(peers[q] + off, __builtin_bit_cast(double, (int64_t)s), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // ---------------------------------------------------------------------------------------------
 // Sweep kernel
 // ---------------------------------------------------------------------------------------------
@@ -1746,18 +1791,12 @@ __device__ __forceinline__ void sweep_body(const SweepArgs& a) {
   // issued after the hand-off's ticket and never waited for (the tail never reads them).  Was: the
   // whole cust_store between the partial and the drain — two round trips per workgroup, +8.5% per
   // stored sweep at c4 / c5.
-  // The sharded fused-exchange instances (FX, world size > 1) keep round 3's placement — the whole
-  // cust_store before the hand-off's drain: with the stores after the ticket, the two-process
-  // rehearsal of c4 on one GPU (tools/gpu_rehearse_n2.sh) timed out in the peer exchange twice in
-  // two runs, with this placement it ran (0.112 ms per sweep) — kept until it is understood.
   const bool has_store = !a.init && cu.active;
-  constexpr bool EARLY = FX;
-  if (EARLY && has_store) cust_store<D, K>(cu, out, a, c, s, stored, true);
   SumsPre<D> pre;
-  const bool pre_sums = !EARLY && !REPLAY && has_store && stored && a.sums != nullptr;
+  const bool pre_sums = !REPLAY && has_store && stored && a.sums != nullptr;
   if (pre_sums) prefetch_sums<D>(a, c, cu.i, pre);
   auto finish_store = [&]() {
-    if (!EARLY && has_store) cust_store<D, K>(cu, out, a, c, s, stored, true, pre_sums ? &pre : nullptr);
+    if (has_store) cust_store<D, K>(cu, out, a, c, s, stored, true, pre_sums ? &pre : nullptr);
   };
   if (!a.fuse) finish_store();
 
@@ -1860,7 +1899,10 @@ __device__ __forceinline__ void sweep_body(const SweepArgs& a) {
         const double* q0 = h0 ? p0 : mb;
         const double* q1 = h1 ? p1 : mb;
         __shared__ uint32_t s_fx_abort;
-        if (threadIdx.x == 0) s_fx_abort = 0;
+        if (threadIdx.x == 0) {
+          s_fx_abort = 0;
+          post_progress(a, a.peers, s);
+        }
         __syncthreads();
         // statistics in chunks of FXC (all NS at once for small NS): the polled values of a chunk
         // and the lane's finished sums are live together, not 2 NS polled values (c5: NS = 34)
@@ -1882,8 +1924,22 @@ __device__ __forceinline__ void sweep_body(const SweepArgs& a) {
               }
             }
             if (__all(ok)) break;
-            if (wait_expired(a, t0, poll)) timed_out = true;
-            else __builtin_amdgcn_s_sleep(1);
+            if (wait_expired(a, t0, poll)) {
+              timed_out = true;
+              int64_t mu_ = -1;
+              int mj = -1;
+              uint64_t mb = 0;
+#pragma unroll
+              for (int q = FXC - 1; q >= 0; --q) {  // the lane's first missing slot
+                if (j0 + q < NS) {
+                  if (h1 && !slot_full(v1[q])) { mu_ = u1; mj = j0 + q; mb = dbits(v1[q]); }
+                  if (h0 && !slot_full(v0[q])) { mu_ = u0; mj = j0 + q; mb = dbits(v0[q]); }
+                }
+              }
+              report_wait(a, WAIT_FX_MAIL, s, c, ok, mu_, mj, mb, poll, t0);
+            } else {
+              __builtin_amdgcn_s_sleep(1);
+            }
           }
 #pragma unroll
           for (int q = 0; q < FXC; ++q) {
@@ -2053,6 +2109,9 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
     const double* q1 = m1 ? p1 : mb;
     double w0[NS], w1[NS];
     bool mdone = !(m0 || m1);  // this lane's mail slots all full (or none to read)
+    if constexpr (P2P) {
+      if (tid == 0) post_progress(a, s_peers, s);
+    }
     {  // each wavefront polls on its own (no barrier per poll); a lane stops once its slots are full.
        // P2P: the mail is polled alongside (the other ranks' units of the last rank to finish are
        // then already in registers when its own partials are complete)
@@ -2085,6 +2144,15 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
         }
         if (__all(done)) break;
         if (wait_expired(a, t0, poll)) {
+          int64_t mb_ = -1;
+          int mj = -1;
+          uint64_t mbits = 0;
+#pragma unroll
+          for (int j = NS - 1; j >= 0; --j) {  // the lane's first missing block partial
+            if (hb1 && !slot_full(v1[j])) { mb_ = b1; mj = j; mbits = dbits(v1[j]); }
+            if (hb0 && !slot_full(v0[j])) { mb_ = b0; mj = j; mbits = dbits(v0[j]); }
+          }
+          report_wait(a, WAIT_BLOCKS, s, c, done, mb_, mj, mbits, poll, t0);
           s_abort = 1;
           break;
         }
@@ -2166,6 +2234,15 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
         }
         if (__all(mdone)) break;
         if (wait_expired(a, tw, poll)) {
+          int64_t mu_ = -1;
+          int mj = -1;
+          uint64_t mbits = 0;
+#pragma unroll
+          for (int j = NS - 1; j >= 0; --j) {  // the lane's first missing unit partial
+            if (m1 && !slot_full(w1[j])) { mu_ = u1; mj = j; mbits = dbits(w1[j]); }
+            if (m0 && !slot_full(w0[j])) { mu_ = u0; mj = j; mbits = dbits(w0[j]); }
+          }
+          report_wait(a, WAIT_P2P_MAIL, s, c, mdone, mu_, mj, mbits, poll, tw);
           s_abort = 1;
           break;
         }
@@ -2332,8 +2409,8 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
   if (tid < HS) Hs[tid] = a.hyper[(int64_t)c * HS + tid];  // sweep s_first: from before this launch
   __syncthreads();
   if (cu.active) cust_ztau<D, K, false>(cu, a, s_first, k0, k1, nullptr, exp_tab);
-  // MH variates drawn ahead (while the wave waits for the level-2 draw) when S fits the registers
-  const bool pre = a.pre_variates && g.S <= PRE_STEPS;
+  // MH variates drawn ahead (while the wave waits for the level-2 draw) when S fits the LDS pool
+  const bool pre = g.S <= PRE_STEPS;
   const PreVariates pv{(float2*)pool, (float*)(pool + PRE_STEPS * BLOCK * 8), tid};
   if (cu.active && pre) mh_pre_variates(SlotPhilox(k0, k1, cu.gi, (uint32_t)s_first), g.S, pv);
   if constexpr (D == 3) {
@@ -2367,6 +2444,7 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
             break;
           }
           if (wait_expired(a, t0, poll)) {
+            report_wait(a, WAIT_HYPER, s, c, slot_full(v), b, tid, dbits(v), poll, t0);
             if (tid == 0) s_abort = 1;
             break;
           }
@@ -2468,7 +2546,8 @@ __global__ void debug_philox_kernel(uint32_t k0, uint32_t k1, const uint32_t* ct
 }
 
 __global__ void debug_variates_kernel(uint64_t seed, int chain, uint32_t sweep, int64_t n, int S, float* tl,
-                                      float* tm, float* ua, double* uz, double* ut, double* ea, double* ez) {
+                                      float* tm, float* ua, float* l2u, double* uz, double* ut, double* ea,
+                                      double* ez) {
   __shared__ __attribute__((aligned(16))) double tab[FAST_TAB_N3];
   fast_tab_fill(tab, threadIdx.x, blockDim.x, true);
   __syncthreads();
@@ -2487,6 +2566,55 @@ __global__ void debug_variates_kernel(uint64_t seed, int chain, uint32_t sweep, 
     tl[(int64_t)j * n + i] = t3_f32(uf32(r.x), angle_hi(r.z));
     tm[(int64_t)j * n + i] = t3_f32(uf32(r.y), angle_lo(r.z));
     ua[(int64_t)j * n + i] = uf32(r.w);
+    l2u[(int64_t)j * n + i] = log2_f32(uf32(r.w));  // the accept threshold's log2 U, as mh_chunk_variates forms it
+  }
+}
+
+// The accept threshold's log2_f32(uf32(w)) (v_log_f32) against fp64 log2 of the same fp32 uniform
+// over the words [w_begin, w_end): per block the max error in fp32 ulps of the exact value, the max
+// absolute error, the word of the max ulp error and the max ulp error where U <= 1/2.
+__global__ void debug_log2u_scan_kernel(uint64_t w_begin, uint64_t w_end, double* out) {
+  double mu = 0.0, ma = 0.0, wu = 0.0, mf = 0.0;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t w = w_begin + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < w_end; w += stride) {
+    const float u = uf32((uint32_t)w);
+    const float y = log2_f32(u);
+    const double e = log2((double)u);
+    double err_ulp;
+    if (e == 0.0) {
+      err_ulp = y == 0.0f ? 0.0 : 1e30;
+    } else {
+      const double ulp = ldexp(1.0, ilogb(e) - 23);  // fp32 ulp at the exact value
+      err_ulp = fabs((double)y - e) / ulp;
+    }
+    const double ae = fabs((double)y - e);
+    if (err_ulp > mu) {
+      mu = err_ulp;
+      wu = (double)w;
+    }
+    ma = fmax(ma, ae);
+    if (u <= 0.5f) mf = fmax(mf, err_ulp);
+  }
+  __shared__ double red[4][256];
+  red[0][threadIdx.x] = mu;
+  red[1][threadIdx.x] = ma;
+  red[2][threadIdx.x] = wu;
+  red[3][threadIdx.x] = mf;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double bm = 0.0, ba = 0.0, bw = 0.0, bf = 0.0;
+    for (int t = 0; t < 256; ++t) {
+      if (red[0][t] > bm) {
+        bm = red[0][t];
+        bw = red[2][t];
+      }
+      ba = fmax(ba, red[1][t]);
+      bf = fmax(bf, red[3][t]);
+    }
+    out[4 * blockIdx.x] = bm;
+    out[4 * blockIdx.x + 1] = ba;
+    out[4 * blockIdx.x + 2] = bw;
+    out[4 * blockIdx.x + 3] = bf;
   }
 }
 
@@ -2700,10 +2828,15 @@ hipError_t launch_debug_philox(uint32_t k0, uint32_t k1, const uint32_t* ctr, in
 }
 
 hipError_t launch_debug_variates(uint64_t seed, int chain, uint32_t sweep, int64_t n, int S, float* tl,
-                                 float* tm, float* ua, double* uz, double* ut, double* ea, double* ez,
+                                 float* tm, float* ua, float* l2u, double* uz, double* ut, double* ea, double* ez,
                                  hipStream_t st) {
   hipLaunchKernelGGL(debug_variates_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, seed, chain,
-                     sweep, n, S, tl, tm, ua, uz, ut, ea, ez);
+                     sweep, n, S, tl, tm, ua, l2u, uz, ut, ea, ez);
+  return hipGetLastError();
+}
+
+hipError_t launch_debug_log2u_scan(uint64_t w_begin, uint64_t w_end, int n_blocks, double* out, hipStream_t st) {
+  hipLaunchKernelGGL(debug_log2u_scan_kernel, dim3((unsigned)n_blocks), dim3(256), 0, st, w_begin, w_end, out);
   return hipGetLastError();
 }
 

@@ -35,19 +35,21 @@ VERIFY_WAIT_MS = 500.0  # in-kernel wait bound while the peer exchange is checke
 
 def run_wait_ms() -> float:
     """The wait bound afterwards: clv_create's default with peers (10 s) or CLV_WAIT_TIMEOUT_MS,
-    parsed as clv_create parses it (C atof: the longest numeric prefix, 0 if none; at least 1 ms),
-    so a value clv_create accepted never raises here."""
+    under clv_create's rule (capi.hip parse_wait_ms): a finite decimal number of ms, blanks around
+    it allowed, clamped to [1 ms, 1 h]; anything else (hex, inf, nan, trailing text) is rejected —
+    clv_create fails on it, so this raises ValueError."""
     import os
     import re
     v = os.environ.get("CLV_WAIT_TIMEOUT_MS")
     if v is None:
         return 10000.0
-    m = re.match(r"\s*[+-]?(\d+\.?\d*|\.\d+)([eE][+-]?\d+)?", v)
-    try:
-        ms = float(m.group(0)) if m else 0.0
-    except ValueError:
-        ms = 0.0
-    return max(1.0, ms) if ms == ms else 1.0
+    t = v.strip(" \t\n")
+    if not re.fullmatch(r"[+-]?(\d+\.?\d*|\.\d+)([eE][+-]?\d+)?", t):
+        raise ValueError(f"CLV_WAIT_TIMEOUT_MS must be a finite decimal number of ms (got {v!r})")
+    ms = float(t)
+    if ms != ms or abs(ms) > 1e300:
+        raise ValueError(f"CLV_WAIT_TIMEOUT_MS must be a finite decimal number of ms (got {v!r})")
+    return min(3.6e6, max(1.0, ms))
 
 
 def graph_sizes_all(chunk: int) -> list:

@@ -306,13 +306,36 @@ class HipSampler:
         return int(self._L.clv_replay_sweep_stride(self.h))
 
     # ---- outputs
-    def read_draws(self, level1: bool = True):
+    def level1_buffer(self) -> np.ndarray:
+        """An uninitialised host array in the level-1 layout [chain][draw][n][D+2] (reference:
+        bi:360-364), for stream_draws / read_draws(out=...)."""
+        return np.empty((self.chains, self.n_draws, self.n, self.D + 2))
+
+    def stream_draws(self, level1: Optional[np.ndarray]) -> None:
+        """clv_stream_draws: copy the level-1 draws into ``level1`` while the sampler runs (host copy
+        pool, overlapped with later sweeps); read_draws(out=level1) then only finishes the copy.
+        ``None`` stops streaming."""
+        if level1 is not None:
+            C, nd, n, D = self.chains, self.n_draws, self.n, self.D
+            if level1.shape != (C, nd, n, D + 2) or level1.dtype != np.float64 or not level1.flags.c_contiguous:
+                raise ValueError("level1 must be a C-contiguous float64 array of shape (chains, n_draws, n, D+2)")
+        self._stream_buf = level1  # kept alive while the library writes into it
+        check(self._L.clv_stream_draws(self.h, dptr(level1)))
+
+    def read_draws(self, level1: bool = True, out: Optional[np.ndarray] = None):
         C, nd, n, D, K = self.chains, self.n_draws, self.n, self.D, self.K
-        l1 = np.empty((C, nd, n, D + 2)) if (level1 and self.draw_sink == "full") else None
+        l1 = None
+        if level1 and self.draw_sink == "full":
+            l1 = out if out is not None else self.level1_buffer()
         l2 = np.empty((C, nd, D * K + D * (D + 1) // 2))
         ll = np.empty((C, nd))
         check(self._L.clv_read_draws(self.h, dptr(l1), dptr(l2), dptr(ll)))
         return l1, l2, ll
+
+    def flush(self) -> None:
+        """Draw a pending deferred level-2 draw now (clv_get_state with only the hyper output)."""
+        hyp = np.empty((self.chains, self.K * self.D + self.D * self.D))
+        check(self._L.clv_get_state(self.h, None, None, dptr(hyp)))
 
     def read_summary(self):
         sums = np.empty((self.chains, _lib.N_SUM_STATS, self.n))  # also for "summary+pct"
@@ -497,8 +520,13 @@ def fit(p: Problem, *, mcmc: int, burnin: int, thin: int, chains: int, seed, tra
             if replay_tape is None:
                 raise ValueError("rng='replay' needs replay_tape")
             s.set_replay_tape(replay_tape, replay_sweeps)
+        l1 = None
+        if draw_sink == "full" and s.n_draws > 0 and p.N > 0:
+            # the draws reach the returned arrays while later sweeps run (clv_stream_draws)
+            l1 = s.level1_buffer()
+            s.stream_draws(l1)
         run_with_trace(s, burnin + mcmc, trace, n_chains_label=chains)
-        l1, l2, ll = s.read_draws(level1=draw_sink == "full")
+        l1, l2, ll = s.read_draws(level1=draw_sink == "full", out=l1)
         sums, k = s.read_summary() if draw_sink in ("summary", "summary+pct") else (None, 0)
         return _assemble(p.D, chains, l1, l2, ll, sums, k, s.n_draws, draw_sink,
                          lambda: s.level1_summary(_lib.SUMMARY_MU_CAP))

@@ -54,10 +54,10 @@ def test_device_variates_match_oracle(L):
     """u53 uniforms bit-exact; fp64 transforms <= 1e-13 rel; fp32 hardware-transcendental
     transforms (t3 noise) <= 2e-5 rel/abs (v_log/v_sin/v_cos/v_rsq are ~1-2 ulp fp32)."""
     n, S, seed, chain, sweep = 4096, 7, 987654321, 2, 77  # one full and one partial 4-step chunk
-    tl, tm, ua = (np.zeros(n * S, np.float32) for _ in range(3))
+    tl, tm, ua, l2u = (np.zeros(n * S, np.float32) for _ in range(4))
     uz, ut, ea, ez = (np.zeros(n) for _ in range(4))
     assert L.clv_debug_variates(seed, chain, sweep, n, S, _fp(tl), _fp(tm), _fp(ua), _dp(uz), _dp(ut), _dp(ea),
-                                _dp(ez)) == 0
+                                _dp(ez), _fp(l2u)) == 0
     ref = oph.sweep_variates(seed, chain, sweep, n, S)
     assert np.array_equal(uz, ref["u_z"]) and np.array_equal(ut, ref["u_tau"])
     np.testing.assert_allclose(ea, ref["e_alive"], rtol=1e-13, atol=0)
@@ -65,6 +65,25 @@ def test_device_variates_match_oracle(L):
     np.testing.assert_array_equal(ua.reshape(S, n), ref["u_acc"])
     np.testing.assert_allclose(tl.reshape(S, n), ref["t_l"], rtol=2e-5, atol=2e-5)
     np.testing.assert_allclose(tm.reshape(S, n), ref["t_m"], rtol=2e-5, atol=2e-5)
+    # the accept threshold's log2 U (v_log_f32 of the same fp32 uniform), to fp32 rounding
+    np.testing.assert_allclose(l2u.reshape(S, n), np.log2(ref["u_acc"].astype(np.float64)), rtol=2**-22, atol=2**-24)
+
+
+def test_accept_log2u_over_every_word(L):
+    """Verdict r4 #4: the accept threshold's log2 U is v_log_f32 of uf32(w) (philox.h log2_f32),
+    checked on the device against float64 log2 of the same fp32 uniform for ALL 2^32 Philox words
+    (clv_debug_log2u_scan).  Bound: <= 1 fp32 ulp of the exact value wherever U <= 1/2, and an
+    absolute error <= 2^-24 everywhere (near U = 1, where log2 U -> 0, the hardware log's error is
+    absolute).  In the accept test exp(lp' - lp) > U (bi:329-330), taken as lp' - lp > ln2 log2 U in
+    fp64, an absolute error e in log2 U scales the acceptance ratio by 2^e: |e| <= 2^-24 is a
+    6e-8 relative change, far below what test_shipped_mh_step_preserves_the_target can see."""
+    out = np.zeros(4)
+    assert L.clv_debug_log2u_scan(0, 1 << 32, _dp(out)) == 0
+    max_ulp, max_abs, worst_word, max_ulp_far = out
+    print(f"log2 U over 2^32 words: max {max_ulp:.3f} ulp (word {int(worst_word):#010x}), "
+          f"max abs {max_abs:.3e}, max {max_ulp_far:.3f} ulp where U <= 1/2")
+    assert max_ulp_far <= 1.0, out
+    assert max_abs <= 2.0 ** -24, out
 
 
 def test_device_hyper_variates_match_oracle(L):

@@ -520,36 +520,49 @@ def test_sharded_step_replays_graphs_for_20_sweeps():
     assert st.graph[16].n == 1 and st.graph[4].n == 2 and st.graph[1].n == 1 and st.s.done == 25
 
 
-@pytest.mark.parametrize("val,want", [(None, 10000.0), ("300", 300.0), ("0.5", 1.0), ("abc", 1.0), ("", 1.0),
-                                      ("  250ms", 250.0), ("1e3", 1000.0), ("-5", 1.0)])
+@pytest.mark.parametrize("val,want", [(None, 10000.0), ("300", 300.0), ("0.5", 1.0), ("  250 ", 250.0),
+                                      ("1e3", 1000.0), ("-5", 1.0), ("1e9", 3.6e6), ("abc", None), ("", None),
+                                      ("250ms", None), ("inf", None), ("nan", None), ("-inf", None), ("0x10", None)])
 def test_run_wait_ms_parses_like_clv_create(monkeypatch, val, want):
-    """the wait bound restored after the peer-path check is parsed as clv_create parses
-    CLV_WAIT_TIMEOUT_MS (atof prefix, clamped to >= 1 ms), so no accepted value raises there."""
+    """CLV_WAIT_TIMEOUT_MS is a finite decimal number of ms clamped to [1 ms, 1 h]
+    (capi.hip parse_wait_ms); inf / nan / hex / trailing text are rejected — by clv_create (EINVAL)
+    and here (ValueError) alike, so no value reaches the kernel's (uint64_t)(ms * 1e5)."""
     from mcmc_clv_model_amd.distributed import run_wait_ms
     if val is None:
         monkeypatch.delenv("CLV_WAIT_TIMEOUT_MS", raising=False)
     else:
         monkeypatch.setenv("CLV_WAIT_TIMEOUT_MS", val)
-    assert run_wait_ms() == want
+    if want is None:
+        with pytest.raises(ValueError):
+            run_wait_ms()
+    else:
+        assert run_wait_ms() == want
 
 
 def test_bench_config_times_the_stored_phase(monkeypatch):
-    """Verdict r3 #3: the c4 / c5 lines time a burn-in window AND a window of stored sweeps (the
-    running-sum read-modify-write of bi:402-428, summary sink), continuing the same chains past the
-    burn-in, and combine both into the whole BASELINE run's rate.  Stub sampler, no GPU."""
+    """Verdict r3 #3 / r4 #1, #5: a configuration leg times a burn-in window AND a window of stored
+    sweeps (the running-sum read-modify-write of bi:402-428, summary sink), continuing the same
+    chains past the burn-in, each with a roofline from an event-timed pass over further sweeps
+    (bound and its evidence printed), both byte accountings (summary sink +0; the
+    kernel's own incl. the sums' read-modify-write), and the whole BASELINE run's rate.  Stub
+    sampler, no GPU."""
     import torch
 
     import bench
     from mcmc_clv_model_amd import sampler as S
 
     log = []
+    timing = []
 
     class Fake:
+        n = 500
+
         def __init__(self, p, **kw):
             self.kw, self.done = kw, 0
+            self.t = False
 
         def run(self, n):
-            log.append((self.done + 1, self.done + n))
+            log.append((self.done + 1, self.done + n, self.t))
             self.done += n
 
         def synchronize(self):
@@ -557,6 +570,14 @@ def test_bench_config_times_the_stored_phase(monkeypatch):
 
         def launch_info(self):
             return dict(persistent=False)
+
+        def set_timing(self, on):
+            self.t = on
+            timing.append(on)
+
+        def kernel_time(self):
+            n = sum(b - a + 1 for a, b, t in log if t)
+            return dict(sweep_ms=0.085 * n, sweep_launches=n, hyper_ms=0.0, hyper_launches=0)
 
         def close(self):
             pass
@@ -566,17 +587,42 @@ def test_bench_config_times_the_stored_phase(monkeypatch):
     monkeypatch.setattr(torch.cuda, "synchronize", lambda *a, **k: None)
     monkeypatch.setitem(bench.WORKLOADS, "c4", bench.WORKLOADS["c4"][:1] + ("synthetic:500:5:20250718",)
                         + bench.WORKLOADS["c4"][2:])
-    r = bench.measure_config("c4", 1, 0, 0, None, 1000, 200, 0, "rccl")
+    r = bench.run_leg("c4", 1, 0, 0, None, 1000, 200)
     burnin = bench.WORKLOADS["c4"][4]
-    assert log == [(1, 200), (201, 1200), (1201, burnin + 100), (burnin + 101, burnin + 1100)]
+    assert [(a, b) for a, b, _ in log] == [(1, 200), (201, 1200), (1201, 2200), (2201, burnin + 100),
+                                           (burnin + 101, burnin + 1100), (burnin + 1101, burnin + 2100)]
+    assert [t for _, _, t in log] == [False, False, True, False, False, True]  # events only on the roofline passes
     assert r["phase"].startswith("burn-in") and r["stored"]["sweeps"] == f"{burnin + 101}..{burnin + 1100}"
     D, K = 2, 5
-    assert r["bytes_per_unit"] == round(bench.algorithmic_bytes(D, K, 0.0, "summary"), 2) == 84.0
-    assert r["stored"]["bytes_per_unit"] == 84.0 + 144.0
+    assert r["bytes_per_unit"] == round(bench.survey_bytes(D, K, 0.0, "summary"), 2) == 84.0
+    assert r["stored"]["bytes_per_unit"] == 84.0  # the summary sink adds 0
+    assert r["stored"]["bytes_per_unit_kernel"] == 84.0 + 144.0
+    roof = r["roofline"]
+    assert roof["bound"] in ("hbm", "valu", "latency", "unmeasured") and "rule" in roof["bound_evidence"]
+    assert abs(roof["launch_us"] - 85.0) < 1e-6 and roof["sweeps_per_launch"] == 1
+    assert abs(roof["achieved"] - 84.0 * 500 / 85e-6 / 1e9) < 1e-3
+    assert r["stored"]["roofline"]["bound"] is not None
     tb, ts = r["ms_per_step"], r["stored"]["ms_per_step"]
     n = 500
     want = n * 10000 / (5000 * tb + 5000 * ts) * 1e3
     assert abs(r["whole_run"]["value"] / want - 1) < 1e-9
     log.clear()
-    r1 = bench.measure_config("c4", 1, 0, 0, None, 1000, 200, 0, "rccl", stored_phase=False)
-    assert log == [(1, 200), (201, 1200)] and "stored" not in r1
+    r1 = bench.run_leg("c4", 1, 0, 0, None, 1000, 200, stored_phase=False)
+    assert [(a, b) for a, b, _ in log] == [(1, 200), (201, 1200), (1201, 2200)] and "stored" not in r1
+
+
+def test_bench_primary_is_a_baseline_configuration():
+    """Verdict r4 #7: the line's `value` is a BASELINE configuration at every N — c2 (configs[1]) on
+    one GPU, the 8-GPU weak-scaling c5 (configs[4]) at N > 1 — and the other configurations run as
+    `configs` legs (N = 1: c3, c4, c5; N > 1: c4 strong scaling and c2 tiled per rank, labelled
+    non-BASELINE in the line)."""
+    import bench
+    assert bench.primary_workload(1) == "c2" and bench.BASELINE_INDEX["c2"] == 1
+    for n in (2, 4, 8):
+        assert bench.primary_workload(n) == "c5" and bench.BASELINE_INDEX["c5"] == 4
+        assert bench.config_legs(n, "c5") == ["c4", "c2"]
+    assert bench.config_legs(1, "c2") == ["c3", "c4", "c5"]
+    assert bench.survey_bytes(2, 2, 0.1, "full") == pytest.approx(63.2) and \
+        bench.survey_bytes(3, 3, 0.1, "full") == pytest.approx(96.0)
+    assert bench.survey_bytes(2, 5, 1.0, "summary") == 84.0 and bench.survey_bytes(3, 9, 1.0, "summary") == 140.0
+    assert bench.survey_bytes(2, 1, 1.0, "full") == 84.0

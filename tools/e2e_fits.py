@@ -50,13 +50,14 @@ def main():
             walls.append(time.perf_counter() - t0)
             assert all(np.isfinite(a).all() for a in d["level_1"])
             lines = out.getvalue().splitlines()
+            rec_bytes, rec_ll = int(sum(a.nbytes for a in d["level_1"])), float(d["log_likelihood"])
+            del d  # freeing the previous call's multi-GB result is not the next call's cost
         sweeps = kw["burnin"] + kw["mcmc"]
         n = len(df)
         rec = dict(fit=name, n_customers=n, covariates=covs, sweeps=sweeps, **kw, seed=42, trace=1000,
                    wall_s=round(walls[1], 4), wall_first_call_s=round(walls[0], 4),
                    customer_sweeps_per_s=kw["chains"] * n * sweeps / walls[1],
-                   level1_bytes=int(sum(a.nbytes for a in d["level_1"])), trace_lines=len(lines),
-                   log_likelihood=float(d["log_likelihood"]))
+                   level1_bytes=rec_bytes, trace_lines=len(lines), log_likelihood=rec_ll)
         if name in PUBLISHED_S:
             rec["published_s"] = PUBLISHED_S[name]
             rec["speedup_vs_published"] = round(PUBLISHED_S[name] / walls[1], 1)
