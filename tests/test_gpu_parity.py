@@ -250,6 +250,71 @@ def test_storage_indexing_and_summary_sink(L):
         assert np.array_equal(bits(summ["level_2"][c]), bits(full["level_2"][c]))
 
 
+@pytest.mark.parametrize("persistent", ["1", "0"])
+def test_streamed_draws_bitwise_equal_read_after_run(L, monkeypatch, persistent):
+    """Verdict r4 #3: level-1 draws streamed into the host buffer while the sampler runs
+    (clv_stream_draws: the stored sweeps in sub-runs, each sub-run's draws copied by the host pool
+    while the next runs) equal, bit for bit, the draws of the same run read after it — through a run
+    cut into uneven calls (one call spans the burn-in boundary and several sub-runs) that stops one
+    sweep short of the last stored draw (its slot is zeros in both), persistent kernel and
+    launch-per-sweep kernel alike; level-2 records and log-likelihood too."""
+    from mcmc_clv_model_amd.sampler import HipSampler, build_problem
+    monkeypatch.setenv("CLV_PERSISTENT", persistent)
+    p = build_problem(cdnow("abe"), ["first_sales_scaled"], 2)
+    kw = dict(mcmc=600, burnin=300, thin=1, chains=3, seed=11, draw_sink="full")
+    calls = (100, 450, 349)
+    with HipSampler(p, **kw) as s:
+        assert s.launch_info()["persistent"] == (persistent == "1")
+        s.run(sum(calls))
+        ref = s.read_draws()
+    with HipSampler(p, **kw) as s:
+        buf = s.level1_buffer()
+        buf.fill(np.nan)
+        s.stream_draws(buf)
+        for n in calls:
+            s.run(n)
+        got = s.read_draws(out=buf)
+    assert got[0] is buf
+    assert not ref[0][:, -1].any()  # the draw never stored: zeros
+    for a, b in zip(ref, got):
+        assert np.array_equal(bits(a), bits(b))
+
+
+def test_stream_draws_arguments(L):
+    """clv_stream_draws needs the full sink; the end-to-end drop-in (which streams) returns the same
+    draws as the sampler read after its run."""
+    from mcmc_clv_model_amd import mcmc_draw_parameters
+    from mcmc_clv_model_amd.sampler import HipSampler, build_problem
+    df = cdnow("abe", 700)
+    p = build_problem(df, [], 2)
+    with HipSampler(p, mcmc=8, burnin=2, thin=2, chains=2, seed=5, draw_sink="summary") as s:
+        with pytest.raises(Exception, match="CLV_SINK_FULL"):
+            s.stream_draws(np.empty((2, 4, 700, 4)))
+    with HipSampler(p, mcmc=8, burnin=2, thin=2, chains=2, seed=5) as s:
+        with pytest.raises(ValueError):
+            s.stream_draws(np.empty((2, 4, 700, 3)))
+        s.run(10)
+        l1, l2, ll = s.read_draws()
+    d = mcmc_draw_parameters(df, mcmc=8, burnin=2, thin=2, chains=2, seed=5, trace=0)
+    for c in range(2):
+        assert np.array_equal(bits(d["level_1"][c]), bits(l1[c])) and np.array_equal(bits(d["level_2"][c]), bits(l2[c]))
+
+
+@pytest.mark.parametrize("val", ["inf", "nan", "0x10", "5 ms"])
+def test_wait_timeout_env_rejected(L, monkeypatch, val):
+    """a CLV_WAIT_TIMEOUT_MS that is not a finite decimal number fails clv_create (EINVAL)
+    instead of reaching (uint64_t)(ms * 1e5); a finite one is clamped to [1 ms, 1 h]."""
+    from mcmc_clv_model_amd.sampler import HipSampler, build_problem
+    p = build_problem(cdnow("abe", 600), [], 2)
+    monkeypatch.setenv("CLV_WAIT_TIMEOUT_MS", val)
+    with pytest.raises(ValueError, match="CLV_WAIT_TIMEOUT_MS"):
+        HipSampler(p, mcmc=2, burnin=0, thin=1, chains=1, seed=1)
+    monkeypatch.setenv("CLV_WAIT_TIMEOUT_MS", "1e12")
+    with HipSampler(p, mcmc=2, burnin=0, thin=1, chains=1, seed=1) as s:
+        assert s.launch_info()["persistent"]
+        s.run(2)
+
+
 def test_edge_cases(L):
     """Single customer, zero-MH-step sweeps, all-zero repeat customers, maximum K=9/D=3."""
     from mcmc_clv_model_amd import mcmc_draw_parameters, mcmc_draw_parameters_rfm_m
