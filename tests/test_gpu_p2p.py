@@ -327,6 +327,11 @@ def test_p2p_abort_leaves_state_unchanged_and_rollback(monkeypatch, persistent):
         sums_before = shards[0].read_summary()[0].copy()
         errs = run_all(4, ranks=[0])  # rank 1 never launches: rank 0's first wait times out
         assert len(errs) == 1 and isinstance(errs[0], _lib.ClvError) and "state unchanged" in str(errs[0])
+        # the wait record names the missing peer unit and the ranks' progress: rank 0 polls for
+        # sweep 4, rank 1's level-2 side last polled for sweep 3 (it never started sweep 4)
+        msg = str(errs[0])
+        assert "[wait record: sweep 4, chain " in msg and "peer unit partial" in msg, msg
+        assert "(rank 1, local unit" in msg and "0:4 1:3" in msg, msg
         assert shards[0].sweeps_done == 3
         after = shards[0].get_state()
         assert all(np.array_equal(bits(x), bits(y)) for x, y in zip(before, after))

@@ -9,6 +9,7 @@
 #                                                                           -> gpurun_out/rehearse_n2.log
 #   profile:W  rocprofv3 trace + PMC passes of workload W (tools/gpu_profile_round.sh W)
 #   stalls:W   the stall / issue counters of workload W (tools/gpu_pmc_stalls.sh W)
+#   stamps:W   one sweep's in-kernel timeline of workload W (diagnostic library libclvmcmc_stamps.so)
 # Usage: tools/gpu_session.sh tests driver e2e
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R; mkdir -p gpurun_out; export TMPDIR=/tmp
 for step in "$@"; do
@@ -38,6 +39,13 @@ for step in "$@"; do
         --master-port 29517 bench.py --gpus 2 --steps ${STEPS:-20} --warmup 5 --one-gpu-rehearsal ${BENCH_ARGS} \
         > gpurun_out/rehearse_n2.log 2>&1; rc=$?
       echo rehearse_rc=$rc; grep -v Warning gpurun_out/rehearse_n2.log | tail -c 2500
+      [ $rc -eq 0 ] || exit $rc ;;
+    stamps:*)
+      # the diagnostic library (make -C mcmc_clv_model_amd/csrc STAMPS=1): one sweep's timeline
+      W=${step#stamps:}
+      case $W in c4|c5) T=tools/stamp_breakdown.py ;; *) T=tools/persist_breakdown.py ;; esac
+      timeout -k 10 300 python $T $W > gpurun_out/stamps_$W.txt 2>&1; rc=$?
+      echo stamps_${W}_rc=$rc; tail -45 gpurun_out/stamps_$W.txt
       [ $rc -eq 0 ] || exit $rc ;;
     profile:*)
       bash tools/gpu_profile_round.sh ${step#profile:} || exit $? ;;
