@@ -5,10 +5,11 @@
 // hipMemcpy after the run (~10 GB/s, the destination's pages faulted in by the copying thread)
 // cost more than all 20,000 sweeps.  Here the copy is spread over the run and off its path:
 //   * a process-wide pool of host worker threads per device, each with its own pinned staging
-//     buffer, sharing ONE non-blocking copy stream (a stream per worker took HIP hardware queues
-//     from the process: two persistent grids of one process on one card then shared a queue and
-//     serialised, tests/test_gpu_p2p.py) — each worker waits for its own copy by an event, and
-//     the DMA of one worker overlaps the memcpy of the others;
+//     buffer, copying on the device's null stream (no stream of the pool's own: a stream holds one
+//     of the process's few HIP hardware queues for good, and persistent grids of one process that
+//     share a queue serialise — tests/test_gpu_p2p.py); the samplers launch on non-blocking
+//     streams, which the null stream does not wait for.  Each worker waits for its own copy by an
+//     event, and the DMA of one worker overlaps the memcpy of the others;
 //   * when a destination is registered (clv_stream_draws) the workers first touch its pages (the
 //     page faults and zeroing happen during the burn-in, in parallel);
 //   * every clv_run hands the draws its sweeps completed to the pool (capi.hip stream_enqueue) and
@@ -45,7 +46,7 @@ struct Piece {
 
 struct Pool {
   int device = 0;
-  hipStream_t st = nullptr;  // the pool's one copy stream (created with the pool)
+  hipStream_t st = nullptr;  // the null stream (see the file comment)
   std::mutex m;
   std::condition_variable cv;
   std::deque<Piece> q;
@@ -55,7 +56,7 @@ struct Pool {
     (void)hipSetDevice(device);
     hipEvent_t ev = nullptr;
     char* stage = nullptr;
-    const bool ok = st && hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess &&
+    const bool ok = hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess &&
                     hipHostMalloc((void**)&stage, STAGE_BYTES, hipHostMallocDefault) == hipSuccess;
     for (;;) {
       Piece p;
@@ -98,11 +99,6 @@ Pool* pool_for(int device) {
     if (p->device == device) return p;
   auto* p = new Pool();
   p->device = device;
-  int prev = -1;
-  (void)hipGetDevice(&prev);
-  (void)hipSetDevice(device);
-  if (hipStreamCreateWithFlags(&p->st, hipStreamNonBlocking) != hipSuccess) p->st = nullptr;  // (workers then fail)
-  if (prev >= 0) (void)hipSetDevice(prev);
   const unsigned hc = std::max(2u, std::thread::hardware_concurrency());
   const int n = (int)std::min(8u, hc / 2);
   for (int k = 0; k < n; ++k) {
