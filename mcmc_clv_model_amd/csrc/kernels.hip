@@ -2457,6 +2457,7 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
     CLV_P_STAMP(a.stamps, wgi, 1, stp);
     StatGen<D, K> st{};
     CustOut<D> out{};
+    if (a.mh_prio) __builtin_amdgcn_s_setprio(2);  // the sweep's critical phase: up to the partial
     if (cu.active) {
       cust_coeffs<D, K, false>(cu, Hs, exp_tab);
       CLV_P_STAMP(a.stamps, wgi, 2, stp);
@@ -2483,6 +2484,7 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
     }
 #endif
     if (tid < NS) st_wt(parts + (int64_t)b * NS + tid, tot[tid]);  // one contiguous 8*NS-byte record
+    if (a.mh_prio) __builtin_amdgcn_s_setprio(0);  // drawing ahead for the next sweep: yield
     CLV_P_STAMP(a.stamps, wgi, 5, stp);
     CLV_P_STAMP(a.stamps, wgi, 8, stp);
     CLV_P_STAMP(a.stamps, wgi, 9, stp);

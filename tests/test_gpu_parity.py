@@ -72,18 +72,18 @@ def test_device_variates_match_oracle(L):
 def test_accept_log2u_over_every_word(L):
     """Verdict r4 #4: the accept threshold's log2 U is v_log_f32 of uf32(w) (philox.h log2_f32),
     checked on the device against float64 log2 of the same fp32 uniform for ALL 2^32 Philox words
-    (clv_debug_log2u_scan).  Bound: <= 1 fp32 ulp of the exact value wherever U <= 1/2, and an
-    absolute error <= 2^-24 everywhere (near U = 1, where log2 U -> 0, the hardware log's error is
-    absolute).  In the accept test exp(lp' - lp) > U (bi:329-330), taken as lp' - lp > ln2 log2 U in
-    fp64, an absolute error e in log2 U scales the acceptance ratio by 2^e: |e| <= 2^-24 is a
-    6e-8 relative change, far below what test_shipped_mh_step_preserves_the_target can see."""
+    (clv_debug_log2u_scan): within 1 fp32 ulp of the exact value everywhere — near U = 1 as well,
+    where log2 U -> 0 (measured on MI355X: max 0.99975 ulp; absolute error <= 0.5 ulp of 33, 1.9e-6,
+    at U ~ 2^-33).  In the accept test exp(lp' - lp) > U (bi:329-330), taken as lp' - lp >
+    ln2 log2 U in fp64, an error e in log2 U scales the acceptance ratio by 2^e, |e| <= 2^-23 |log2 U|
+    <= 4e-6: far below what test_shipped_mh_step_preserves_the_target resolves (2^0.02)."""
     out = np.zeros(4)
     assert L.clv_debug_log2u_scan(0, 1 << 32, _dp(out)) == 0
     max_ulp, max_abs, worst_word, max_ulp_far = out
-    print(f"log2 U over 2^32 words: max {max_ulp:.3f} ulp (word {int(worst_word):#010x}), "
-          f"max abs {max_abs:.3e}, max {max_ulp_far:.3f} ulp where U <= 1/2")
-    assert max_ulp_far <= 1.0, out
-    assert max_abs <= 2.0 ** -24, out
+    print(f"log2 U over 2^32 words: max {max_ulp:.5f} ulp (word {int(worst_word):#010x}), "
+          f"max abs {max_abs:.3e}, max {max_ulp_far:.5f} ulp where U <= 1/2")
+    assert max_ulp <= 1.0, out
+    assert max_ulp_far <= 1.0 and max_abs <= 0.5 * 2.0 ** (5 - 23), out
 
 
 def test_device_hyper_variates_match_oracle(L):
