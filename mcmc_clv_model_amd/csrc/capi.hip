@@ -79,7 +79,6 @@ SweepArgs sweep_args(clv_sampler* s, int init, int fuse = 0) {
   a.wait_ticks = s->wait_ticks;
   a.abort_host = s->d_h_abort;
   a.diag = s->d_diag;
-  a.mh_prio = s->mh_prio;
   a.h = hyper_args(s, nullptr, 0);
   if (fuse) a.h.hvar = s->replay ? nullptr : s->d_hvar;
   return a;
@@ -362,9 +361,7 @@ namespace {
 // chain's level-2 workgroup (asleep most of the time) shares a CU with one of its own customer
 // workgroups, and the pairs are spread evenly over the chains.  Pure placement: every workgroup
 // still runs one logical (chain, block), so results do not depend on it.
-// cross (A/B): shared CUs pair chain c with chain c + C/2 instead (C even), for a wave-priority
-// schedule in which one chain's MH phase runs beside the other's drawing-ahead phase.
-std::vector<int32_t> persist_wg_map(int C, int nb, int n_cu, bool cross = false) {
+std::vector<int32_t> persist_wg_map(int C, int nb, int n_cu) {
   const int per = nb + 1;  // workgroups per chain (block nb = the level-2 workgroup)
   const int T = C * per;
   std::vector<int32_t> map(T);
@@ -372,36 +369,27 @@ std::vector<int32_t> persist_wg_map(int C, int nb, int n_cu, bool cross = false)
     for (int b = 0; b < per; ++b) map[c * per + b] = (c << 16) | b;
   const int P = T - n_cu;  // shared CUs
   if (P <= 0 || T > 2 * n_cu) return map;
-  if (C < 2 || C % 2) cross = false;
-  auto partner = [&](int c) { return cross ? (c + C / 2) % C : c; };
   std::vector<std::vector<int>> todo(C);  // customer blocks of each chain still to place
   for (int c = 0; c < C; ++c)
     for (int b = nb - 1; b >= 0; --b) todo[c].push_back(b);
   std::vector<int32_t> first, second, single;
   int p = 0;
-  for (int c = 0; c < C && p < P; ++c, ++p) {  // level-2 workgroup + one customer workgroup of the partner
+  for (int c = 0; c < C && p < P; ++c, ++p) {  // level-2 workgroup + one own customer workgroup
     first.push_back((c << 16) | nb);
-    const int q = partner(c);
-    if (todo[q].empty()) return map;
-    second.push_back((q << 16) | todo[q].back());
-    todo[q].pop_back();
+    if (todo[c].empty()) return map;
+    second.push_back((c << 16) | todo[c].back());
+    todo[c].pop_back();
   }
   const bool l2_paired = (int)first.size() == C;
-  const int n_lead = cross ? C / 2 : C;  // chains that lead a pair
-  for (int c = 0; p < P; c = (c + 1) % n_lead) {  // customer pairs, round robin over the leading chains
-    auto can = [&](int k) {
-      const int q = partner(k);
-      return q == k ? todo[k].size() >= 2 : (!todo[k].empty() && !todo[q].empty());
-    };
+  for (int c = 0; p < P; c = (c + 1) % C) {  // same-chain customer pairs, round robin over chains
     bool any = false;
-    for (int k = 0; k < n_lead && !any; ++k) any = can((c + k) % n_lead);
-    if (!any) return map;  // cannot pair: keep the identity
-    if (!can(c)) continue;
+    for (int k = 0; k < C && !any; ++k) any = todo[(c + k) % C].size() >= 2;
+    if (!any) return map;  // cannot pair within chains: keep the identity
+    if (todo[c].size() < 2) continue;
     first.push_back((c << 16) | todo[c].back());
     todo[c].pop_back();
-    const int q = partner(c);
-    second.push_back((q << 16) | todo[q].back());
-    todo[q].pop_back();
+    second.push_back((c << 16) | todo[c].back());
+    todo[c].pop_back();
     ++p;
   }
   for (int c = 0; c < C; ++c) {
@@ -621,15 +609,12 @@ int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* pri
     }
     s->wait_ticks = (uint64_t)(ms * 1e5);  // s_memrealtime: 100 MHz
   }
-  // (A/B, round 5) CLV_WG_PAIRING = same | cross | none, CLV_MH_PRIO = 0 | 1
-  const char* pairing = std::getenv("CLV_WG_PAIRING");
-  const std::string pmode = pairing ? pairing : (g.D == 2 ? "same" : "none");
-  if (const char* e = std::getenv("CLV_MH_PRIO")) s->mh_prio = std::atoi(e);
-  if ((s->persistent || s->p2p_capable) && s->n_cu > 0 && pmode != "none") {
-    // the bivariate model only: measured c2 13.44 -> 12.94 us per sweep, but c3 (trivariate: longer
-    // level-2 draw, so both waves of a same-chain pair idle in the hand-off together) 16.36 -> 17.31
+  if ((s->persistent || s->p2p_capable) && s->n_cu > 0) {
+    // same-chain pairs on shared CUs, bivariate and trivariate: with the MH-phase wave priority
+    // (kernels.hip persist_kernel) measured c2 10.70 -> 9.58 us per sweep against no map, c3 11.45 ->
+    // 11.1 (chain pairs c / c + 2 instead: c2 10.16, c3 11.1; profiles/r05_ab_priority.txt)
     {
-      std::vector<int32_t> map = persist_wg_map((int)C, (int)nb_local, s->n_cu, pmode == "cross");
+      std::vector<int32_t> map = persist_wg_map((int)C, (int)nb_local, s->n_cu);
       CLV_HIPC(dalloc(&s->d_wgmap, map.size()));
       CLV_HIPC(hipMemcpy(s->d_wgmap, map.data(), sizeof(int32_t) * map.size(), hipMemcpyHostToDevice));
     }

@@ -135,7 +135,6 @@ struct clv_sampler {
   int mail_kind = -1;               // the mail's memory: 0 uncached, 1 fine-grained, 2 plain device memory
   double** d_peers = nullptr;       // [world] mail pointers (peers' opened IPC mappings, own d_mail)
   int32_t* d_wgmap = nullptr;       // persistent grid: linear workgroup -> (chain << 16 | block)
-  int mh_prio = 0;                  // persistent customer waves: raised priority in the MH phase
   std::vector<void*> ipc_opened;    // hipIpcOpenMemHandle mappings to close
   double* d_hvar = nullptr;         // [chain][HV] precomputed hyper variates
   unsigned long long* d_stamps = nullptr;  // CLV_STAMPS diagnostic build only

@@ -139,7 +139,6 @@ struct SweepArgs {
   // wait expires claims word 0 and writes what it was waiting for (kernels.hip report_wait); the
   // host formats it into clv_last_error()
   unsigned long long* diag;
-  int mh_prio;               // persistent kernel: customer waves at priority 2 from (beta, Sigma) to the partial
   HyperArgs h;               // level-2 arguments of the fused tail
   unsigned long long* stamps; // diagnostic build only (CLV_STAMPS): [1024][8] s_memrealtime stamps
 };

@@ -1776,7 +1776,6 @@ __device__ __forceinline__ void sweep_body(const SweepArgs& a) {
       // are independent of the state, so they are generated while the current chunk's fp64
       // accept/reject chain runs (ILP for the ~1.5 waves/SIMD of the CDNOW-sized problem).
       if (threadIdx.x == 0) CLV_WG_STAMP(a.stamps, (int64_t)c * g.nb_local + b, 5);
-      if (a.mh_prio & 2) __builtin_amdgcn_s_setprio(2);  // (A/B) the MH phase ahead of loads / z-tau
       mh_run(cu, SlotPhilox(k0, k1, cu.gi, (uint32_t)s), s00, s11, g.S, exp_tab);
     }
     if (threadIdx.x == 0) CLV_WG_STAMP(a.stamps, (int64_t)c * g.nb_local + b, 6);
@@ -1787,7 +1786,6 @@ __device__ __forceinline__ void sweep_body(const SweepArgs& a) {
   if (threadIdx.x < NS)  // sc1 (write-through) store: read cross-CU by the fused tail
     __hip_atomic_store(a.blockpart + ((int64_t)c * g.stride + threadIdx.x) * g.blocks_per_rank + b, tot[threadIdx.x],
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (a.mh_prio & 2) __builtin_amdgcn_s_setprio(0);
   // draws / summaries / state: the running sums' loads go out with the partial's store, so the
   // hand-off's drain below waits for both in one memory round trip; the sums' and draws' stores are
   // issued after the hand-off's ticket and never waited for (the tail never reads them).  Was: the
@@ -1843,7 +1841,6 @@ __device__ __forceinline__ void sweep_body(const SweepArgs& a) {
         finish_store();
         return;
       }
-      if (a.mh_prio & 4) __builtin_amdgcn_s_setprio(3);  // (A/B) the unit's and the chain's tail
       if (threadIdx.x < NS) {  // unit partial: sequential over the unit's blocks (= group_kernel)
         const double* p = a.blockpart + ((int64_t)c * g.stride + threadIdx.x) * g.blocks_per_rank + (int64_t)u * bpu;
         double t = 0.0;
@@ -1886,7 +1883,6 @@ __device__ __forceinline__ void sweep_body(const SweepArgs& a) {
     // wait for these stores in vmcnt order, measured 0.5-1.2 us per sweep slower at c4, round 4)
     finish_store();
     if (s_last) {
-      if (a.mh_prio & 4) __builtin_amdgcn_s_setprio(3);
       if (threadIdx.x == 0) CLV_STAMP(a.stamps, s, 2, false);
       if (!fx) {
         hyper_body<D, K, REPLAY, NS, NT>(a.h, c, s, 0, units, red, tot, var_iw, var_chi, var_noise, &l2);
@@ -2461,7 +2457,13 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
     CLV_P_STAMP(a.stamps, wgi, 1, stp);
     StatGen<D, K> st{};
     CustOut<D> out{};
-    if (a.mh_prio & 1) __builtin_amdgcn_s_setprio(2);  // the sweep's critical phase: up to the partial
+    // Wave priority by phase (round 5): from (beta, Sigma) of sweep s to its block partial a customer
+    // wave is on the chain's critical path (the level-2 draw waits for the last partial), after it
+    // the wave only draws ahead for sweep s + 1.  A SIMD holding two customer waves (c2: 464 of
+    // 1,024) used to split its issue between one wave's MH phase and the other's drawing ahead by
+    // age; the critical phase now goes first (the level-2 workgroup keeps priority 3):
+    // c2 10.62 -> 9.58 us per sweep, c3 12.37 -> 11.1 (tools/ab_env.sh, profiles/r05_ab_priority.txt).
+    __builtin_amdgcn_s_setprio(2);
     if (cu.active) {
       cust_coeffs<D, K, false>(cu, Hs, exp_tab);
       CLV_P_STAMP(a.stamps, wgi, 2, stp);
@@ -2488,7 +2490,7 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
     }
 #endif
     if (tid < NS) st_wt(parts + (int64_t)b * NS + tid, tot[tid]);  // one contiguous 8*NS-byte record
-    if (a.mh_prio & 1) __builtin_amdgcn_s_setprio(0);  // drawing ahead for the next sweep: yield
+    __builtin_amdgcn_s_setprio(0);  // drawing ahead for the next sweep: yield the SIMD
     CLV_P_STAMP(a.stamps, wgi, 5, stp);
     CLV_P_STAMP(a.stamps, wgi, 8, stp);
     CLV_P_STAMP(a.stamps, wgi, 9, stp);
