@@ -1626,14 +1626,10 @@ __device__ __forceinline__ void cust_store(const Cust<D, K, CL>& u, const CustOu
 static_assert(BLOCK == EXP_TAB_N, "the sweep kernel stages the exp table with one entry per lane");
 
 // A head launch's customer wave (its active lanes) after z / tau: wait for the head workgroup's
-// ready word for sweep s; the hyper state the head wrote (write-through stores, drained before the
-// ready word) is then read with plain loads.  No cache of this launch can hold an older copy of
-// chain c's hyper state: the launch's acquire invalidated the CU caches, the device-local memory
-// (MTYPE RW) is kept coherent between the XCDs' L2s by probes, and no wave reads chain c's state
-// before its ready word.  (An agent-scope acquire here — buffer_inv sc1 by every wave — measured
-// c4 83 -> 150 us per sweep.)  The workgroup-scope fence orders the compiler only.  A wait that
-// expires leaves the wait record and the abort flag (clv_run fails the call); the wave goes on, so
-// the workgroup's barriers are all reached.
+// ready word for sweep s, then an agent-scope acquire, so the hyper state it wrote during this
+// launch on another CU is what the loads that follow read (no stale line of an earlier launch).  A
+// wait that expires leaves the wait record and the abort flag (clv_run fails the call); the wave
+// goes on, so the workgroup's barriers are all reached.
 __device__ __forceinline__ void wait_head_draw(const SweepArgs& a, int c, int64_t s, int b) {
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   for (uint32_t poll = 0;; ++poll) {
@@ -1645,7 +1641,7 @@ __device__ __forceinline__ void wait_head_draw(const SweepArgs& a, int c, int64_
     }
     __builtin_amdgcn_s_sleep(1);
   }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 }
 
 // FX: the fused peer exchange (world size > 1 after clv_p2p_connect) compiled in — instances of
