@@ -79,9 +79,6 @@ SweepArgs sweep_args(clv_sampler* s, int init, int fuse = 0) {
   a.wait_ticks = s->wait_ticks;
   a.abort_host = s->d_h_abort;
   a.diag = s->d_diag;
-  a.head = 0;
-  a.defer = 0;
-  a.ready = s->d_ready;
   a.h = hyper_args(s, nullptr, 0);
   if (fuse) a.h.hvar = s->replay ? nullptr : s->d_hvar;
   return a;
@@ -126,16 +123,10 @@ int enqueue_sweep(clv_sampler* s, hipEvent_t e0, hipEvent_t e1) {
   return CLV_OK;
 }
 
-// One launch per sweep; the level-2 draw runs in the sweep kernel's tail, or (head draws) in the
-// next launch's head workgroup.  k of n: this launch's place in a run of consecutive launches.
-int enqueue_fused(clv_sampler* s, hipEvent_t e0, hipEvent_t e1, int64_t k = 0, int64_t n = 1) {
+// world_size == 1: one launch per sweep (the level-2 draw runs in the sweep kernel's tail)
+int enqueue_fused(clv_sampler* s, hipEvent_t e0, hipEvent_t e1) {
   s->last_persist_n = 0;
-  SweepArgs a = sweep_args(s, 0, 1);
-  if (s->head_draw && s->g.world_size == 1) {
-    a.head = k > 0 ? 1 : 0;
-    a.defer = k < n - 1 ? 1 : 0;
-  }
-  CLV_HIP(launch_sweep(a, s->replay, s->stream, e0, e1));
+  CLV_HIP(launch_sweep(sweep_args(s, 0, 1), s->replay, s->stream, e0, e1));
   return CLV_OK;
 }
 
@@ -186,7 +177,7 @@ int build_graph(clv_sampler* s, int n) {
   hipGraph_t graph;
   CLV_HIP(hipStreamBeginCapture(s->stream, hipStreamCaptureModeThreadLocal));
   for (int k = 0; k < n; ++k) {
-    int rc = enqueue_fused(s, nullptr, nullptr, k, n);
+    int rc = enqueue_fused(s, nullptr, nullptr);
     if (rc != CLV_OK) {
       hipGraph_t dummy;
       (void)hipStreamEndCapture(s->stream, &dummy);
@@ -242,13 +233,9 @@ std::string take_wait_diag(clv_sampler* s) {
   const Geometry& g = s->g;
   const char* what = d[1] == WAIT_HYPER ? "(beta, Sigma) hand-off slot"
                      : d[1] == WAIT_BLOCKS ? "block partial"
-                     : d[1] == WAIT_P2P_MAIL ? "peer unit partial (persistent)"
-                     : d[1] == WAIT_FX_MAIL ? "peer unit partial (fused)" : "head draw's ready word";
+                     : d[1] == WAIT_P2P_MAIL ? "peer unit partial (persistent)" : "peer unit partial (fused)";
   std::string m = std::string(" [wait record: sweep ") + std::to_string((long long)d[2]) + ", chain " +
                   std::to_string(d[3]) + ", rank " + std::to_string(d[4]) + ": " + what + " ";
-  if (d[1] == WAIT_HEAD)  // (customer block d[5]; the word read, as a signed sweep index)
-    return m + "at block " + std::to_string((long long)d[5]) + ": read " + std::to_string((long long)d[7]) +
-           " after " + std::to_string(d[8]) + " polls, " + std::to_string(d[9] / 100000.0) + " ms]";
   const long long unit = (long long)d[5];
   if ((d[1] == WAIT_P2P_MAIL || d[1] == WAIT_FX_MAIL) && g.units_per_rank > 0 && unit >= 0)
     m += "unit " + std::to_string(unit) + " (rank " + std::to_string(unit / g.units_per_rank) + ", local unit " +
@@ -607,25 +594,13 @@ int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* pri
     CLV_HIPC(dalloc(&s->d_hyper_alt, C * HS));
     if ((cfg->draw_sink == CLV_SINK_SUMMARY || cfg->draw_sink == CLV_SINK_SUMMARY_PCT) && n > 0)
       CLV_HIPC(dalloc(&s->d_sums_prev, (size_t)C * CLV_N_SUM_STATS * n));
-  }
-  // World size 1 without the persistent kernel: head draws (CLV_DEFER=0: every launch draws in its
-  // own tail)
-  if (cfg->world_size == 1 && !s->persistent && nb_local > 0) {
-    const char* env = std::getenv("CLV_DEFER");
-    s->head_draw = !(env && std::string(env) == "0");
-    if (s->head_draw) {
-      CLV_HIPC(dalloc(&s->d_ready, C));
-      CLV_HIPC(hipMemsetAsync(s->d_ready, 0xFF, sizeof(int64_t) * C, s->stream));  // -1: none published
-    }
-  }
-  if (s->persistent || s->p2p_capable || s->fx_capable || s->head_draw) {  // bounded waits
     CLV_HIPC(dalloc(&s->d_diag, DIAG_WORDS));
     CLV_HIPC(hipMemsetAsync(s->d_diag, 0, sizeof(unsigned long long) * DIAG_WORDS, s->stream));
     CLV_HIPC(hipHostMalloc((void**)&s->h_abort, sizeof(uint32_t), hipHostMallocMapped));
     *s->h_abort = 0;
     CLV_HIPC(hipHostGetDevicePointer((void**)&s->d_h_abort, s->h_abort, 0));
-    // every wait is bounded: 2 s at world size 1 (the awaited workgroups are resident, so a wait
-    // that long means a fault), 10 s with peers (host-side launch skew between
+    // every wait of the persistent kernel is bounded: 2 s at world size 1 (all workgroups are
+    // resident, so a wait that long means a fault), 10 s with peers (host-side launch skew between
     // ranks); CLV_WAIT_TIMEOUT_MS overrides
     double ms = cfg->world_size > 1 ? 10000.0 : 2000.0;
     if (const char* env = std::getenv("CLV_WAIT_TIMEOUT_MS")) {
@@ -754,8 +729,7 @@ void clv_destroy(clv_sampler* s) {
   if (s->d_unit && s->d_unit != s->d_block) (void)hipFree(s->d_unit);
   if (s->d_hyp2) (void)hipFree(s->d_hyp2);
   for (void* p : {(void*)s->d_lam_alt, (void*)s->d_mu_alt, (void*)s->d_hyper_alt, (void*)s->d_sums_prev,
-                  (void*)s->d_pblock, (void*)s->d_qstore, (void*)s->d_pend, (void*)s->d_diag,
-                  (void*)s->d_ready})
+                  (void*)s->d_pblock, (void*)s->d_qstore, (void*)s->d_pend, (void*)s->d_diag})
     if (p) (void)hipFree(p);
   if (s->h_abort) (void)hipHostFree(s->h_abort);
   for (void* p : s->ipc_opened) (void)hipIpcCloseMemHandle(p);
@@ -858,7 +832,7 @@ int clv_launch_info(const clv_sampler* s, int64_t* out) {
   out[1] = s->persist_bpc;
   out[2] = s->n_cu;
   out[3] = (int64_t)(s->g.nb_local + (s->persistent ? 1 : 0)) * s->g.n_chains;
-  out[4] = s->head_draw ? 1 : 0;  // launch per sweep: level-2 draws in the next launch's head
+  out[4] = 0;  // (reserved: was the MH-variate producer / consumer chunks, removed in round 4)
   out[5] = 0;  // (reserved: was the stride kernel's grid, removed)
   return CLV_OK;
 }
@@ -1115,9 +1089,9 @@ int enqueue_fused_sweeps(clv_sampler* s, int64_t n_sweeps) {
   if (s->timing) {
     rc = ensure_events(s);
     if (rc) return rc;
-    for (int64_t q = 0; q < n_sweeps; ++q) {
+    while (left > 0) {
       const int k = s->ev_used;
-      rc = enqueue_fused(s, s->ev[4 * k], s->ev[4 * k + 1], q, n_sweeps);
+      rc = enqueue_fused(s, s->ev[4 * k], s->ev[4 * k + 1]);
       if (rc) return rc;
       s->ev_used++;
       s->sweeps_done++;
@@ -1138,22 +1112,13 @@ int enqueue_fused_sweeps(clv_sampler* s, int64_t n_sweeps) {
       left -= GRAPH_CHUNK;
     }
   }
-  for (int64_t q = 0, m = left; q < m; ++q) {
-    rc = enqueue_fused(s, nullptr, nullptr, q, m);
+  while (left > 0) {
+    rc = enqueue_fused(s, nullptr, nullptr);
     if (rc) return rc;
     s->sweeps_done++;
     left--;
   }
   return CLV_OK;
-}
-
-// After a world-size-1 run of launches: a head workgroup's wait that expired (a fault) fails the
-// call with the wait record.  The sampler's state is then undefined.
-int check_head_abort(clv_sampler* s) {
-  if (!s->head_draw || !s->h_abort || !__atomic_load_n(s->h_abort, __ATOMIC_ACQUIRE)) return CLV_OK;
-  *s->h_abort = 0;
-  CLV_HIP(hipMemset(&s->d_ctrl->abort, 0, sizeof(uint32_t)));
-  return fail(CLV_EHIP, "level-2 head draw: a wait timed out; sampler state undefined" + take_wait_diag(s));
 }
 
 // World size > 1 without a resident grid: n launches of the sweep kernel whose fused tail
@@ -1216,7 +1181,6 @@ int run_streaming(clv_sampler* s, int64_t n_sweeps) {
     } else {
       rc = enqueue_fused_sweeps(s, k);
       if (rc == CLV_OK && hipStreamSynchronize(s->stream) != hipSuccess) rc = fail(CLV_EHIP, "hipStreamSynchronize");
-      if (rc == CLV_OK) rc = check_head_abort(s);
     }
     if (rc) return rc;
     stream_enqueue(s);
@@ -1258,7 +1222,7 @@ int clv_run(clv_sampler* s, int64_t n_sweeps) {
   rc = enqueue_fused_sweeps(s, n_sweeps);
   if (rc) return rc;
   CLV_HIP(hipStreamSynchronize(s->stream));
-  return check_head_abort(s);
+  return CLV_OK;
 }
 
 int clv_stream_draws(clv_sampler* s, double* level1) {

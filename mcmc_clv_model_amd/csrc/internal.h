@@ -125,13 +125,6 @@ struct clv_sampler {
   bool rb_pend = false;             // rollback: the pending state before the last persistent launch
   int rb_pend_buf = 0;
   int rb_hyper_swaps = 0;           // hyper / hyper_alt swaps since it (its hyper is in hyper_alt if odd)
-  // Head draws (world size 1, launch per sweep, CLV_DEFER != "0"): within each run of consecutive
-  // launches (a captured chunk, the launches after it), every launch but the last leaves its level-2
-  // draw to the next launch's head workgroup, which draws while the customer workgroups draw z / tau
-  // (kernels.hip sweep_body, SweepArgs::head).  The last launch of a run draws in its tail, so the
-  // state is complete between calls.  d_ready: [chain] the sweep a head draw published.
-  bool head_draw = false;
-  int64_t* d_ready = nullptr;
   bool persistent = false;          // clv_run uses persist_kernel (all workgroups resident)
   int persist_bpc = 0, n_cu = 0;    // persist_kernel occupancy (workgroups per CU), CUs
   // world size > 1: persistent kernel with the peer (xGMI) exchange

@@ -19,7 +19,7 @@ constexpr int HV = 40;                 // precomputed Philox hyper variates per 
 constexpr int MAIL_TAIL = MAX_WORLD;   // peer mail: after the [2][world][chain][unit][stat] slots, one
                                        // progress word per rank (the sweep its level-2 side last polled for)
 constexpr int DIAG_WORDS = 16;         // wait-timeout record (SweepArgs::diag, see kernels.hip report_wait)
-enum : int { WAIT_HYPER = 1, WAIT_BLOCKS = 2, WAIT_P2P_MAIL = 3, WAIT_FX_MAIL = 4, WAIT_HEAD = 5 };
+enum : int { WAIT_HYPER = 1, WAIT_BLOCKS = 2, WAIT_P2P_MAIL = 3, WAIT_FX_MAIL = 4 };
 
 // Doubles of peer-mail slots before the progress words.
 __host__ __device__ inline int64_t mail_slots(int world, int chains, int stride, int units_per_rank) {
@@ -82,9 +82,7 @@ struct HyperArgs {
   double nu_n;
   double omega2;
   int mode;                  // 0: after sweep (cur+1); 1: bivariate initial draw (sweep 1)
-  const double* hvar;        // [2][chain][HV] Philox variates precomputed by the sweep kernel (by the
-                             // statistics' sweep parity: a head draw reads one while the same launch
-                             // writes the other), or null
+  const double* hvar;        // [chain][HV] Philox variates precomputed by the sweep kernel, or null
   unsigned long long* stamps; // diagnostic build only (CLV_STAMPS)
 };
 
@@ -114,7 +112,7 @@ struct SweepArgs {
   uint32_t* chain_arrive;    // [chain] arrival counters of the fused tail (zero between launches)
   uint32_t* unit_arrive;     // [chain][units_per_rank] per-unit arrival counters (blocks_per_unit > 1)
   double* unitpart;          // [chain][stride][units_per_rank] unit partials (blocks_per_unit > 1)
-  double* hvar_out;          // [2][chain][HV]: the chain's last workgroup precomputes the next level-2
+  double* hvar_out;          // [chain][HV]: the chain's last workgroup precomputes the next level-2
                              // draw's Philox variates at its start (off the critical path), or null
   // persistent kernel at world size > 1 (peer exchange over xGMI): unit partials of sweep s go
   // straight into every rank's mail buffer, [2 (sweep parity)][world][chain][units_per_rank][stride]
@@ -141,14 +139,6 @@ struct SweepArgs {
   // wait expires claims word 0 and writes what it was waiting for (kernels.hip report_wait); the
   // host formats it into clv_last_error()
   unsigned long long* diag;
-  // launch-per-sweep at world size 1 (clv_create CLV_DEFER, capi.hip enqueue_fused): defer = 1: the
-  // chain's last workgroup does not draw (beta, Sigma) from this sweep's statistics — the next
-  // launch does, with head = 1: its grid has one extra workgroup per chain (blockIdx.x 0, dispatched
-  // first) that draws at once and publishes ready[chain] = its sweep, while the customer workgroups
-  // draw z / tau; they wait for it before their MH steps.  ready: [chain] (-1 between launches).
-  int head;
-  int defer;
-  int64_t* ready;
   HyperArgs h;               // level-2 arguments of the fused tail
   unsigned long long* stamps; // diagnostic build only (CLV_STAMPS): [1024][8] s_memrealtime stamps
 };

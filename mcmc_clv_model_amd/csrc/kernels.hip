@@ -336,9 +336,6 @@ __device__ __forceinline__ int64_t uniform_i64(int64_t v) {
   const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)v >> 32));
   return (int64_t)(((uint64_t)hi << 32) | lo);
 }
-__device__ __forceinline__ double uniform_f64(double v) {  // a wave-uniform double into SGPRs
-  return __builtin_bit_cast(double, uniform_i64(__builtin_bit_cast(int64_t, v)));
-}
 
 // s is wave-uniform at every call site and sweep counts are 32-bit (clv_config): the offset is
 // made explicitly uniform so the modulo / division run on the scalar unit (the persistent kernel
@@ -815,13 +812,13 @@ __device__ __forceinline__ void level2_draw(const double* tot, const double* iwn
 }
 
 // Philox-mode hyper variates (fp64).
-__device__ __forceinline__ double hyper_normal(uint32_t k0, uint32_t k1, uint32_t slot, uint32_t sweep) {
+__device__ double hyper_normal(uint32_t k0, uint32_t k1, uint32_t slot, uint32_t sweep) {
   const u32x4 r = hyper_block(k0, k1, slot, sweep);
   return sqrt(-2.0 * log(u53_open0(r.x, r.y))) * cospi(2.0 * u53(r.z, r.w));
 }
 
 // Marsaglia–Tsang Gamma(alpha, 1), alpha >= 1; chi2(df) = 2 Gamma(df / 2).
-__device__ __forceinline__ double chi2_draw(uint32_t k0, uint32_t k1, uint32_t sweep, int idx, double df) {
+__device__ double chi2_draw(uint32_t k0, uint32_t k1, uint32_t sweep, int idx, double df) {
   const double alpha = 0.5 * df;
   const double dd = alpha - 1.0 / 3.0;
   const double cc = 1.0 / sqrt(9.0 * dd);
@@ -836,18 +833,6 @@ __device__ __forceinline__ double chi2_draw(uint32_t k0, uint32_t k1, uint32_t s
     if (lu < 0.5 * x * x + dd * (3.0 * log1p(t) - v1)) return 2.0 * dd * (1.0 + v1);
   }
   return df;  // unreachable in practice (acceptance > 0.95 per attempt)
-}
-
-// Sweep s is complete for one more chain: the last chain to arrive advances the sweep counter
-// (every workgroup of this launch has read it before arriving).  Relaxed: the next launch reads cur
-// and the hyper state after the kernel boundary (whose release/acquire makes them visible); an
-// acq_rel RMW here would write back the whole L2.
-__device__ __forceinline__ void sweep_arrival(Ctrl* ctrl, int n_chains, int64_t s) {
-  const uint32_t old = __hip_atomic_fetch_add(&ctrl->arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (old == (uint32_t)n_chains - 1) {
-    __hip_atomic_store(&ctrl->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&ctrl->cur, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
 }
 
 // Level-2 draw of chain c after sweep s (mode 0), or the bivariate initial draw (mode 1):
@@ -873,7 +858,7 @@ __device__ __forceinline__ void hyper_variates(const HyperArgs& a, int c, int64_
     if (tid < 3) var_chi[tid] = tv[3 + tid];
     if (tid < D * K) var_noise[tid] = tv[6 + tid];
   } else if (a.hvar) {  // precomputed by this sweep's kernel (sc1 stores: read with sc1 loads)
-    const double* hv = a.hvar + ((int64_t)(s & 1) * a.g.n_chains + c) * HV;
+    const double* hv = a.hvar + (int64_t)c * HV;
     if (tid < 3) var_iw[tid] = __hip_atomic_load(hv + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (tid < 3) var_chi[tid] = __hip_atomic_load(hv + 3 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (tid < D * K) var_noise[tid] = __hip_atomic_load(hv + 8 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -971,8 +956,18 @@ __device__ void hyper_finish(const HyperArgs& a, int c, int64_t s, int mode, dou
     }
     if (mode != 1 && is_stored(s, g))
       a.loglik[(int64_t)c * g.n_draws + draw_index(s, g)] = tot[NS - 1] / (double)g.n_global;  // np.mean
-    if (mode == 0) sweep_arrival(a.ctrl, g.n_chains, s);  // (mode 2: the persistent kernel keeps
-  }                                                         // the sweep index itself; a head draw)
+    if (mode == 0) {  // (mode 2, the persistent kernel, keeps the sweep index itself)
+      // the last chain to finish advances the sweep counter (every workgroup of this launch has
+      // read it before arriving)
+      // relaxed: the next launch reads cur and the hyper state after the kernel boundary (whose
+      // release/acquire makes them visible); an acq_rel RMW here would write back the whole L2
+      const uint32_t old = __hip_atomic_fetch_add(&a.ctrl->arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (old == (uint32_t)g.n_chains - 1) {
+        __hip_atomic_store(&a.ctrl->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&a.ctrl->cur, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
 }
 
 // Level-2 draw of chain c after sweep s (mode 0), or the bivariate initial draw (mode 1):
@@ -1004,7 +999,7 @@ __device__ void hyper_body(const HyperArgs& a, int c, int64_t s, int mode, const
     if (tid < 3) w_chi = tv[3 + tid];
     if (tid < D * K) w_noise = tv[6 + tid];
   } else if (a.hvar) {  // precomputed by this sweep's kernel (sc1 stores: read with sc1 loads)
-    const double* hv = a.hvar + ((int64_t)(s & 1) * a.g.n_chains + c) * HV;
+    const double* hv = a.hvar + (int64_t)c * HV;
     if (tid < 3) w_iw = __hip_atomic_load(hv + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (tid < 3) w_chi = __hip_atomic_load(hv + 3 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (tid < D * K) w_noise = __hip_atomic_load(hv + 8 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1625,25 +1620,6 @@ __device__ __forceinline__ void cust_store(const Cust<D, K, CL>& u, const CustOu
 
 static_assert(BLOCK == EXP_TAB_N, "the sweep kernel stages the exp table with one entry per lane");
 
-// A head launch's customer wave (its active lanes) after z / tau: wait for the head workgroup's
-// ready word for sweep s, then an agent-scope acquire, so the hyper state it wrote during this
-// launch on another CU is what the loads that follow read (no stale line of an earlier launch).  A
-// wait that expires leaves the wait record and the abort flag (clv_run fails the call); the wave
-// goes on, so the workgroup's barriers are all reached.
-__device__ __forceinline__ void wait_head_draw(const SweepArgs& a, int c, int64_t s, int b) {
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  for (uint32_t poll = 0;; ++poll) {
-    const int64_t r = __hip_atomic_load(a.ready + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (r == s) break;
-    if (wait_expired(a, t0, poll)) {
-      report_wait(a, WAIT_HEAD, s, c, false, b, -1, (uint64_t)r, poll, t0);
-      break;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-}
-
 // FX: the fused peer exchange (world size > 1 after clv_p2p_connect) compiled in — instances of
 // their own, launched for sharded runs only (compiled into the world-size-1 kernels it cost c4 /
 // c5 1.8% / 1.6% per sweep).
@@ -1656,25 +1632,6 @@ __device__ __forceinline__ void sweep_body(const SweepArgs& a) {
   __shared__ double red[BLOCK / 64][NS];
   __shared__ double tot[NS];
   __shared__ __attribute__((aligned(16))) double exp_tab[D == 3 ? FAST_TAB_N3 : FAST_TAB_N];
-  __shared__ uint32_t s_last;
-  __shared__ double var_iw[4], var_chi[4], var_noise[32];
-  __shared__ L2Scratch l2;
-  const Geometry& g = a.g;
-  const int c = blockIdx.y;
-  // The level-2 draw this workgroup makes after its block, if any: the statistics' sweep (-1: none)
-  // and hyper_body's mode.  One call site for the tail's draw and the head workgroup's (a second
-  // inlined copy raised the bivariate c4 instance from 124 to 168 VGPRs, 4 -> 3 waves per SIMD).
-  int64_t draw_s = -1;
-  int draw_mode = 0;
-  // The head workgroup (a.head): the level-2 draw the previous launch deferred — from that sweep's
-  // unit partials, as its tail would have drawn (the same function, the same sums, the same bits) —
-  // then the ready word.  Dispatched before every customer workgroup of its chain, it never waits.
-  if (!FX && a.head && blockIdx.x == 0) {
-    __builtin_amdgcn_s_setprio(3);  // a one-lane latency chain on CUs full of customer waves
-    draw_s = a.ctrl->cur;
-    draw_mode = 2;
-  } else {
-  const int b = (int)blockIdx.x - (a.head ? 1 : 0);
   // the exp/log(/cos) table's global loads are issued first; they are stored to LDS (and the
   // barrier taken) after the customer's own loads are in flight
   static_assert(BLOCK == EXP_TAB_N && BLOCK == LOG_TAB_N && BLOCK == COS_TAB_N, "one table entry per thread");
@@ -1689,6 +1646,9 @@ __device__ __forceinline__ void sweep_body(const SweepArgs& a) {
     }
   }
 
+  const Geometry& g = a.g;
+  const int c = blockIdx.y;
+  const int b = blockIdx.x;
   if constexpr (FX) {  // a wait of an earlier launch of this call timed out: the call fails, and
                        // its remaining launches return at once (the host restores the state)
     if (a.fuse && g.world_size > 1 &&
@@ -1776,14 +1736,13 @@ __device__ __forceinline__ void sweep_body(const SweepArgs& a) {
         v = chi2_draw(k0, k1, (uint32_t)hs, l - 40, a.h.nu_n - D + 1 + (l - 40));
         slot = 3 + (l - 40);
       }
-      if (slot >= 0)
-        __hip_atomic_store(a.hvar_out + ((int64_t)(s & 1) * g.n_chains + c) * HV + slot, v, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+      if (slot >= 0) __hip_atomic_store(a.hvar_out + (int64_t)c * HV + slot, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 
   CustOut<D> out{};
   if (!a.init && cu.active) {
+    const double* H = a.hyper + (int64_t)c * HS;
     uint32_t k0 = 0, k1 = 0;
     const double* tape = nullptr;
     if constexpr (REPLAY) {
@@ -1791,13 +1750,10 @@ __device__ __forceinline__ void sweep_body(const SweepArgs& a) {
     } else {
       chain_key(a.r.seed, (int64_t)a.r.chain_first + c, &k0, &k1);
     }
-    cust_ztau<D, K, REPLAY>(cu, a, s, k0, k1, tape, exp_tab);  // independent of (beta, Sigma)
-    if (a.head) wait_head_draw(a, c, s, b);
-    const double* H = a.hyper + (int64_t)c * HS;
-    cust_coeffs<D, K, REPLAY>(cu, H, exp_tab);
+    cust_prepare<D, K, REPLAY>(cu, a, c, s, H, k0, k1, tape, exp_tab);
     if (threadIdx.x == 0) CLV_WG_STAMP(a.stamps, (int64_t)c * g.nb_local + b, 9);
-    const double s00 = uniform_f64(H[H_S00]);  // (SGPRs for the MH phase)
-    const double s11 = uniform_f64(H[H_S11]);
+    const double s00 = H[H_S00];
+    const double s11 = H[H_S11];
     if constexpr (REPLAY) {
       {
         auto& u = cu;
@@ -1852,9 +1808,13 @@ __device__ __forceinline__ void sweep_body(const SweepArgs& a) {
   // (write-through), every wave drains its stores, one lane takes an agent-scope ticket; the
   // last arriver reads every handed-off value with sc1 loads (no L1 hit possible).
   if (a.fuse) {
+    __shared__ uint32_t s_last;
+    __shared__ double var_iw[4], var_chi[4], var_noise[32];
+    __shared__ L2Scratch l2;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    const int bpu = g.blocks_per_unit;  // (bpu == 1: a unit is one block)
+    const int bpu = g.blocks_per_unit;
+    const double* units = a.blockpart;  // a unit is one block
     // fused peer exchange (world size > 1, clv_p2p_connect): every unit partial goes straight into
     // every rank's mail, [parity][rank][chain][unit][stat], system-scope write-through stores (the
     // value is its own arrival flag); the chain's last unit on this rank then waits in its own mail
@@ -1900,6 +1860,7 @@ __device__ __forceinline__ void sweep_body(const SweepArgs& a) {
                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       }
+      units = a.unitpart;
     }
     if (bpu > 1 || fx) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1923,13 +1884,8 @@ __device__ __forceinline__ void sweep_body(const SweepArgs& a) {
     finish_store();
     if (s_last) {
       if (threadIdx.x == 0) CLV_STAMP(a.stamps, s, 2, false);
-      if (!fx && a.defer) {  // the next launch's head workgroup draws from these statistics
-        if (threadIdx.x == 0) {
-          __hip_atomic_store(a.ready + c, (int64_t)-1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          sweep_arrival(a.h.ctrl, g.n_chains, s);
-        }
-      } else if (!fx) {
-        draw_s = s;  // (below)
+      if (!fx) {
+        hyper_body<D, K, REPLAY, NS, NT>(a.h, c, s, 0, units, red, tot, var_iw, var_chi, var_noise, &l2);
       } else {
         hyper_variates<D, K, REPLAY>(a.h, c, s, var_iw, var_chi, var_noise, &l2);
         // every rank's units of sweep s from this rank's mail: lane u reads units u, u + NT
@@ -2005,17 +1961,7 @@ __device__ __forceinline__ void sweep_body(const SweepArgs& a) {
           hyper_finish<D, K, REPLAY, NS, NT>(a.h, c, s, 0, acc, red, tot, var_iw, var_chi, var_noise, &l2);
         }
       }
-      if (threadIdx.x == 0 && draw_s < 0) CLV_STAMP(a.stamps, s, 3, false);
-    }
-  }
-  }  // (customer workgroups)
-  if (draw_s >= 0) {
-    const double* units = g.blocks_per_unit > 1 ? a.unitpart : a.blockpart;
-    hyper_body<D, K, REPLAY, NS, NT>(a.h, c, draw_s, draw_mode, units, red, tot, var_iw, var_chi, var_noise, &l2);
-    if (threadIdx.x == 0 && draw_mode == 0) CLV_STAMP(a.stamps, draw_s, 3, false);
-    if (draw_mode == 2 && threadIdx.x == 0) {  // (lane 0 wrote the hyper state: write-through
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stores, drained here)
-      __hip_atomic_store(a.ready + c, draw_s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (threadIdx.x == 0) CLV_STAMP(a.stamps, s, 3, false);
     }
   }
 }
@@ -2035,7 +1981,7 @@ __global__ __launch_bounds__(BLOCK, 4) void sweep_kernel_occ4(SweepArgs a) {
 // One instance per (D, K, REPLAY, FX): the occupancy variant SweepOcc picks (only that one compiled).
 template <int D, int K, bool REPLAY, bool FX>
 hipError_t launch_sweep_t(const SweepArgs& a, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
-  const dim3 grid(a.g.nb_local + (a.head ? 1 : 0), a.g.n_chains);
+  const dim3 grid(a.g.nb_local, a.g.n_chains);
   const dim3 block(BLOCK);
   // e0/e1: hipExtLaunchKernelGGL records the dispatch's own start/end timestamps into the events
   // (no extra marker packets in the stream, unlike hipEventRecord around the launch).

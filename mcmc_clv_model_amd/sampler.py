@@ -254,7 +254,7 @@ class HipSampler:
         out = (ctypes.c_int64 * 6)()
         check(self._L.clv_launch_info(self.h, out))
         return dict(persistent=bool(out[0]), persist_blocks_per_cu=int(out[1]), n_cu=int(out[2]),
-                    workgroups=int(out[3]), head_draw=bool(out[4]))
+                    workgroups=int(out[3]))
 
     # ---- peer exchange (world size > 1 through the persistent kernel, include/clvmcmc.h)
     IPC_HANDLE_BYTES = 64

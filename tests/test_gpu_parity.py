@@ -671,8 +671,6 @@ def _run_ops(p, env, ops, **kw):
                 s.run(op[1])
             elif op[0] == "state":
                 mid.append(s.get_state())
-            elif op[0] == "timing":
-                s.set_timing(bool(op[1]))
             else:
                 s.rollback()
         st = s.get_state()
@@ -714,31 +712,6 @@ def test_deferred_level2_draw_bitwise(L, D, covs, sink):
     a = _run_ops(p, {"CLV_PERSISTENT": "1", "CLV_DEFER": "1"}, rb, **kw)
     b = _run_ops(p, {"CLV_PERSISTENT": "1", "CLV_DEFER": "1"}, straight, **kw)
     _same_bits(a[1:], b[1:])
-
-
-@pytest.mark.parametrize("D,covs,n,sink", [(2, ["first_sales_scaled"], 23570, "full"),
-                                            (3, ["gender_F", "age_scaled"], 23570, "summary"),
-                                            (2, ["c1", "c2", "c3", "c4"], 300000, "summary+pct")])
-def test_head_draw_bitwise(L, D, covs, n, sink):
-    """Launch per sweep at world size 1 (round 5): within a run of launches every launch but the
-    last leaves its level-2 draw to the next launch's head workgroup, which draws it while the
-    customer workgroups draw z / tau (kernels.hip sweep_body, SweepArgs::head).  Bit for bit the run
-    with every draw in its own launch's tail (CLV_DEFER=0): calls covering a captured chunk (64
-    launches) and a remainder, single launches, timed launches (one event pair each) and a state
-    read between calls; the bivariate K = 5 case at 300,000 customers has 4 blocks per unit (the
-    unit partials the head draw sums) and runs the c4 instance (sweep_kernel_occ4<2,5>)."""
-    from mcmc_clv_model_amd.data import synthetic_cbs
-    from mcmc_clv_model_amd.sampler import build_problem
-    df = synthetic_cbs(n, len(covs) + 1, D, seed=n) if covs[0] == "c1" else cdnow("full", n)
-    p = build_problem(df, covs, D)
-    kw = dict(mcmc=100, burnin=59, thin=3, chains=2 if n < 100000 else 1, seed=91, draw_sink=sink)
-    ops = [("run", 1), ("run", 70), ("state",), ("run", 2), ("timing", 1), ("run", 5), ("timing", 0),
-           ("run", 80), ("run", 1)]
-    ref = _run_ops(p, {"CLV_PERSISTENT": "0", "CLV_DEFER": "0"}, ops, **kw)
-    hd = _run_ops(p, {"CLV_PERSISTENT": "0"}, ops, **kw)
-    assert not ref[0]["persistent"] and not ref[0]["head_draw"], ref[0]
-    assert not hd[0]["persistent"] and hd[0]["head_draw"], hd[0]
-    _same_bits(ref[1:], hd[1:])
 
 
 def _mh_step_device(L, f, t3, log_u, cur_pt=None):
