@@ -9,5 +9,5 @@ mkdir -p $R/build/$1
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Wno-unused-variable -Wno-bitwise-instead-of-logical \
   -ffp-contract=off $2 -c $C/kernels.hip -o $R/build/$1/kernels.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $R/build/$1/kernels.o $C/capi.o $C/analysis.o $C/elog.o $C/group.o \
-  -o $R/build/$1/libclvmcmc.so
+  $C/drawstream.o -lpthread -o $R/build/$1/libclvmcmc.so
 echo built build/$1/libclvmcmc.so
