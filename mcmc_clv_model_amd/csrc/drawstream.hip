@@ -10,16 +10,20 @@
 //     share a queue serialise — tests/test_gpu_p2p.py); the samplers launch on non-blocking
 //     streams, which the null stream does not wait for.  Each worker waits for its own copy by an
 //     event, and the DMA of one worker overlaps the memcpy of the others;
-//   * when a destination is registered (clv_stream_draws) the workers first touch its pages (the
-//     page faults and zeroing happen during the burn-in, in parallel);
+//   * when a destination is registered (clv_stream_draws) the workers first fault its pages in
+//     (madvise MADV_POPULATE_WRITE: the page faults and zeroing happen during the burn-in, in
+//     parallel);
 //   * every clv_run hands the draws its sweeps completed to the pool (capi.hip stream_enqueue) and
 //     returns; the copies run while the next sweeps do.  clv_read_draws waits for what is in
 //     flight and copies the rest.
 // The source ranges are draws of completed launches: later launches write other draw indices only.
 #include <hip/hip_runtime.h>
 
+#include <sys/mman.h>
+
 #include <algorithm>
 #include <atomic>
+#include <cstdint>
 #include <condition_variable>
 #include <cstring>
 #include <deque>
@@ -68,9 +72,12 @@ struct Pool {
       }
       bool good = ok;
       if (!p.src) {
-        // first touch of every page (an atomic OR of zero: a concurrent copy into the same page
-        // keeps its bytes whichever lands first)
-        for (size_t off = 0; off < p.bytes; off += PAGE) __atomic_fetch_or(p.dst + off, (char)0, __ATOMIC_RELAXED);
+        // fault every page in, writable, without touching its bytes (the kernel zero-fills only
+        // pages not yet present, so a copy into the same range by another worker is never undone);
+        // where MADV_POPULATE_WRITE is refused, a first touch by an atomic OR of zero instead
+        const uintptr_t b0 = (uintptr_t)p.dst & ~(uintptr_t)(PAGE - 1);
+        if (madvise((void*)b0, (uintptr_t)p.dst + p.bytes - b0, MADV_POPULATE_WRITE) != 0)
+          for (size_t off = 0; off < p.bytes; off += PAGE) __atomic_fetch_or(p.dst + off, (char)0, __ATOMIC_RELAXED);
       } else {
         for (size_t off = 0; good && off < p.bytes; off += STAGE_BYTES) {
           const size_t len = std::min(STAGE_BYTES, p.bytes - off);
