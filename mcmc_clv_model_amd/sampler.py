@@ -317,8 +317,9 @@ class HipSampler:
         ``None`` stops streaming."""
         if level1 is not None:
             C, nd, n, D = self.chains, self.n_draws, self.n, self.D
-            if level1.shape != (C, nd, n, D + 2) or level1.dtype != np.float64 or not level1.flags.c_contiguous:
-                raise ValueError("level1 must be a C-contiguous float64 array of shape (chains, n_draws, n, D+2)")
+            if (level1.shape != (C, nd, n, D + 2) or level1.dtype != np.float64 or not level1.flags.c_contiguous
+                    or not level1.flags.writeable):
+                raise ValueError("level1 must be a writeable C-contiguous float64 array of shape (chains, n_draws, n, D+2)")
         self._stream_buf = level1  # kept alive while the library writes into it
         check(self._L.clv_stream_draws(self.h, dptr(level1)))
 

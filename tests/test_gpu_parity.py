@@ -293,6 +293,10 @@ def test_stream_draws_arguments(L):
     with HipSampler(p, mcmc=8, burnin=2, thin=2, chains=2, seed=5) as s:
         with pytest.raises(ValueError):
             s.stream_draws(np.empty((2, 4, 700, 3)))
+        ro = s.level1_buffer()
+        ro.flags.writeable = False
+        with pytest.raises(ValueError):
+            s.stream_draws(ro)
         s.run(10)
         l1, l2, ll = s.read_draws()
     d = mcmc_draw_parameters(df, mcmc=8, burnin=2, thin=2, chains=2, seed=5, trace=0)
