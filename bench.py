@@ -143,10 +143,16 @@ def committed_counters(workload: str, kname: str, D: int, K: int):
                             valu_active_frac_of_wave_lifetime=round(k["valu_active_frac_of_wave_lifetime"], 4),
                             valu_insts_per_wave=round(k["valu_insts_per_wave"], 1), waves=k["waves"],
                             source=os.path.basename(path))
+                if k["waves"] <= 2 * N_SIMDS:  # a grid resident at once (the persistent kernel): the
+                    # SIMDs holding ceil(waves / SIMDs) waves set the period
+                    per_simd = -(-int(k["waves"]) // N_SIMDS)
+                    best["waves_per_simd_max"] = per_simd
+                    best["valu_busy_frac_max_simd"] = round(busy * per_simd * N_SIMDS / k["waves"], 4)
     return best
 
 
-BOUND_RULE = "hbm if measured HBM traffic >= 0.6 of peak; else valu if VALU busy >= 0.7; else latency"
+BOUND_RULE = ("hbm if measured HBM traffic >= 0.6 of peak; else valu if VALU busy >= 0.7 (for a grid resident at "
+              "once: on the SIMDs holding the most waves); else latency")
 
 
 def load_workload(name: str, world: int = 1):
@@ -277,7 +283,7 @@ def roofline_for(workload: str, kname: str, D: int, K: int, bpu: float, units: i
         ev["hbm_traffic_frac"] = round(r["traffic"] / t_launch / 1e9 / HBM_PEAK_GBS, 4)
     if ev.get("hbm_traffic_frac", 0.0) >= 0.6:
         r["bound"] = "hbm"
-    elif ev.get("valu_busy_frac", 0.0) >= 0.7:
+    elif max(ev.get("valu_busy_frac", 0.0), ev.get("valu_busy_frac_max_simd", 0.0)) >= 0.7:
         r["bound"] = "valu"
     elif "valu_busy_frac" in ev:
         r["bound"] = "latency"
