@@ -211,9 +211,10 @@ int clv_read_draws(clv_sampler* s, double* level1, double* level2, double* logli
  * CLV_SINK_FULL) — the drop-in's end-to-end time, run_mcmc_abe.py:60-77 around bi:437-504, instead
  * of one pageable copy of every stored draw after the run.  level1: [chain][n_draws][n][D+2]
  * doubles, caller-owned, valid until clv_read_draws with the same pointer (or NULL here, or
- * clv_destroy).  Host threads of a process-wide copy pool first touch its pages, then each clv_run
- * (its stored sweeps in sub-runs of >= 256 sweeps and ~64 MB of draws) hands the draws it completed
- * to the pool (pinned staging, DMA on streams of the pool's own) and goes on sampling;
+ * clv_destroy).  Host threads of a process-wide copy pool first fault its pages in (madvise
+ * MADV_POPULATE_WRITE), then each clv_run (its stored sweeps in sub-runs of >= 256 sweeps and ~64 MB
+ * of draws) hands the draws it completed to the pool (pinned staging, DMA on the device's null
+ * stream, which the sampler's non-blocking stream does not wait for) and goes on sampling;
  * clv_read_draws(s, level1, ...) waits for the copies in flight and copies what is left.  Same
  * launches, same sweeps, same bits.  NULL stops streaming (after the copies in flight). */
 int clv_stream_draws(clv_sampler* s, double* level1);
