@@ -374,7 +374,34 @@ __global__ __launch_bounds__(64) void group_kernel(GroupArgs a) {
 // ---------------------------------------------------------------------------------------------
 // Level-2 algebra (bi:243-261) on reduced statistics.
 // ---------------------------------------------------------------------------------------------
-template <int D>
+// Philox mode: the level-2 draw's one-lane chain (Cholesky pivots, the inverse's determinant, the
+// trivariate posterior variance) takes 1/sqrt and 1/x as the hardware estimate (v_rsq_f64 /
+// v_rcp_f64, relative error ~2^-23) refined by two Newton steps (~1 ulp): 7 / 5 dependent VALU
+// instead of the IEEE sqrt / division sequences with their range scaling.  The draw is the serial
+// link of every sweep's hand-off (persistent kernel: publish -> customers -> partials -> draw).
+// Their arguments there are positive normal numbers (S_n's pivots, Sigma's diagonal and
+// determinant).  Replay mode keeps sqrt and '/' (the reference's operations).
+#ifndef CLV_L2_NR
+#define CLV_L2_NR 1
+#endif
+__device__ __forceinline__ double rsq_nr(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const double h = x * y;
+    const double e = __builtin_fma(-h, y, 1.0);  // 1 - x y^2
+    y = __builtin_fma(0.5 * y, e, y);
+  }
+  return y;
+}
+__device__ __forceinline__ double rcp_nr(double x) {
+  double y = __builtin_amdgcn_rcp(x);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) y = __builtin_fma(y, __builtin_fma(-x, y, 1.0), y);
+  return y;
+}
+
+template <int D, bool NR = false>
 __device__ void cholesky(const double (&A)[D][D], double (&L)[D][D]) {
 #pragma unroll
   for (int r = 0; r < D; ++r)
@@ -385,13 +412,14 @@ __device__ void cholesky(const double (&A)[D][D], double (&L)[D][D]) {
     double sdiag = A[j][j];
 #pragma unroll
     for (int k = 0; k < j; ++k) sdiag -= L[j][k] * L[j][k];
-    L[j][j] = sqrt(sdiag);
+    const double rj = NR ? rsq_nr(sdiag) : 0.0;  // NR: sqrt(d) = d / sqrt(d), x / L[j][j] = x rsq(d)
+    L[j][j] = NR ? sdiag * rj : sqrt(sdiag);
 #pragma unroll
     for (int r = j + 1; r < D; ++r) {
       double sv = A[r][j];
 #pragma unroll
       for (int k = 0; k < j; ++k) sv -= L[r][k] * L[j][k];
-      L[r][j] = sv / L[j][j];
+      L[r][j] = NR ? sv * rj : sv / L[j][j];
     }
   }
 }
@@ -411,7 +439,9 @@ __device__ __forceinline__ void hput(double* H, int idx, double v) {
 }
 
 // hyper-state finalisation from (beta, Sigma): inverse block, proposal scales, eta constants.
-template <int D, int K, bool TO_LDS = false>
+// NR (Philox mode): the divisions as products with rcp_nr, sqrt(post_var) as rsq_nr of its
+// reciprocal (the level-2 chain's tail; see rsq_nr).
+template <int D, int K, bool TO_LDS = false, bool NR = false>
 __device__ void finalize_hyper(const double* beta_flat, const double (&Sig)[D][D], double omega2, double* H) {
 #pragma unroll
   for (int q = 0; q < K * D; ++q) hput<TO_LDS>(H, H_BETA + q, beta_flat[q]);
@@ -422,25 +452,48 @@ __device__ void finalize_hyper(const double* beta_flat, const double (&Sig)[D][D
     for (int q = 0; q < D; ++q) hput<TO_LDS>(H, H_SIGMA + p * 3 + q, Sig[p][q]);
   if constexpr (D == 2) {
     const double det = Sig[0][0] * Sig[1][1] - Sig[0][1] * Sig[1][0];
-    hput<TO_LDS>(H, H_P00, Sig[1][1] / det);
-    hput<TO_LDS>(H, H_P01, -Sig[0][1] / det);
-    hput<TO_LDS>(H, H_P11, Sig[0][0] / det);
+    if constexpr (NR) {
+      const double id = rcp_nr(det);
+      hput<TO_LDS>(H, H_P00, Sig[1][1] * id);
+      hput<TO_LDS>(H, H_P01, -Sig[0][1] * id);
+      hput<TO_LDS>(H, H_P11, Sig[0][0] * id);
+    } else {
+      hput<TO_LDS>(H, H_P00, Sig[1][1] / det);
+      hput<TO_LDS>(H, H_P01, -Sig[0][1] / det);
+      hput<TO_LDS>(H, H_P11, Sig[0][0] / det);
+    }
   } else {
     // top-left 2x2 block of the full 3x3 inverse (tri:402 with tri:422-424; quirk Q4)
     const double c00 = Sig[1][1] * Sig[2][2] - Sig[1][2] * Sig[2][1];
     const double c01 = Sig[1][0] * Sig[2][2] - Sig[1][2] * Sig[2][0];
     const double c02 = Sig[1][0] * Sig[2][1] - Sig[1][1] * Sig[2][0];
     const double det = Sig[0][0] * c00 - Sig[0][1] * c01 + Sig[0][2] * c02;
-    hput<TO_LDS>(H, H_P00, c00 / det);
-    hput<TO_LDS>(H, H_P01, -(Sig[0][1] * Sig[2][2] - Sig[0][2] * Sig[2][1]) / det);
-    hput<TO_LDS>(H, H_P11, (Sig[0][0] * Sig[2][2] - Sig[0][2] * Sig[2][0]) / det);
+    const double n01 = -(Sig[0][1] * Sig[2][2] - Sig[0][2] * Sig[2][1]);
+    const double n11 = Sig[0][0] * Sig[2][2] - Sig[0][2] * Sig[2][0];
     hput<TO_LDS>(H, H_S22, Sig[2][2]);
-    const double post_var = 1.0 / (1.0 / omega2 + 1.0 / Sig[2][2]);  // tri:325-326
-    hput<TO_LDS>(H, H_POSTVAR, post_var);
-    hput<TO_LDS>(H, H_SQRT_POSTVAR, sqrt(post_var));
     hput<TO_LDS>(H, H_OMEGA2, omega2);
-    hput<TO_LDS>(H, H_INV_OMEGA2, 1.0 / omega2);
-    hput<TO_LDS>(H, H_INV_S22, 1.0 / Sig[2][2]);
+    if constexpr (NR) {
+      const double id = rcp_nr(det);
+      hput<TO_LDS>(H, H_P00, c00 * id);
+      hput<TO_LDS>(H, H_P01, n01 * id);
+      hput<TO_LDS>(H, H_P11, n11 * id);
+      const double inv_om = 1.0 / omega2;  // (the run's constant: off the chain)
+      const double inv_s22 = rcp_nr(Sig[2][2]);
+      const double prec = inv_om + inv_s22;  // tri:325-326: post_var = 1 / prec
+      hput<TO_LDS>(H, H_POSTVAR, rcp_nr(prec));
+      hput<TO_LDS>(H, H_SQRT_POSTVAR, rsq_nr(prec));
+      hput<TO_LDS>(H, H_INV_OMEGA2, inv_om);
+      hput<TO_LDS>(H, H_INV_S22, inv_s22);
+    } else {
+      hput<TO_LDS>(H, H_P00, c00 / det);
+      hput<TO_LDS>(H, H_P01, n01 / det);
+      hput<TO_LDS>(H, H_P11, n11 / det);
+      const double post_var = 1.0 / (1.0 / omega2 + 1.0 / Sig[2][2]);  // tri:325-326
+      hput<TO_LDS>(H, H_POSTVAR, post_var);
+      hput<TO_LDS>(H, H_SQRT_POSTVAR, sqrt(post_var));
+      hput<TO_LDS>(H, H_INV_OMEGA2, 1.0 / omega2);
+      hput<TO_LDS>(H, H_INV_S22, 1.0 / Sig[2][2]);
+    }
   }
   hput<TO_LDS>(H, H_S00, Sig[0][0]);
   hput<TO_LDS>(H, H_S11, Sig[1][1]);
@@ -631,11 +684,11 @@ __device__ __forceinline__ void bartlett_inverse(const double* iwn, const double
 // Philox-mode core (one lane): Sigma = (L A^-1)(L A^-1)' with L = chol(S_n) — the Bartlett form of
 // level2_draw_exact with A^-1 applied by multiplication instead of a triangular solve.  M = L A^-1
 // is lower triangular with a positive diagonal, so it IS chol(Sigma): no second factorisation.
-template <int D>
+template <int D, bool NR = CLV_L2_NR != 0>
 __device__ __forceinline__ void iw_core_fast(const double (&Sn)[D][D], const double* Ai, double (&Sig)[D][D],
                                              double (&M)[D][D]) {
   double L[D][D];
-  cholesky<D>(Sn, L);
+  cholesky<D, NR>(Sn, L);
 #pragma unroll
   for (int r = 0; r < D; ++r)
 #pragma unroll
@@ -662,7 +715,7 @@ __device__ __forceinline__ void iw_core_fast(const double (&Sn)[D][D], const dou
 // element-parallel phases of level2_draw_exact around the fast core.  `Ai`: the Bartlett inverse
 // if already formed (LDS), else null.  Every path (fused, sharded, persistent) calls this same
 // function in Philox mode, so they stay bitwise identical.
-template <int D, int K, int LANE0_MAX = 12>
+template <int D, int K, int LANE0_MAX = 12, bool NR = CLV_L2_NR != 0>
 __device__ void level2_draw_fast(const double* tot, const double* iwn, const double* chi2, const double* noise,
                                  const double* Ai_pre, L2Scratch* sc) {
   constexpr int NXY = K * D;
@@ -713,7 +766,7 @@ __device__ void level2_draw_fast(const double* tot, const double* iwn, const dou
           Sn[q][p] = Sn[p][q];
         }
       double Sig[D][D], M[D][D];
-      iw_core_fast<D>(Sn, Ai, Sig, M);
+      iw_core_fast<D, NR>(Sn, Ai, Sig, M);
       asm volatile("" ::: "memory");  // chol(V) and the noise are read here, not hoisted above (registers)
       double sv[NXY];
 #pragma unroll
@@ -775,7 +828,7 @@ __device__ void level2_draw_fast(const double* tot, const double* iwn, const dou
           Sn[q][p] = sc->Sn[n++];
         }
       double Sig[D][D], M[D][D];
-      iw_core_fast<D>(Sn, Ai, Sig, M);
+      iw_core_fast<D, NR>(Sn, Ai, Sig, M);
 #pragma unroll
       for (int p = 0; p < D; ++p)
 #pragma unroll
@@ -945,7 +998,7 @@ __device__ void hyper_finish(const HyperArgs& a, int c, int64_t s, int mode, dou
     for (int p = 0; p < D; ++p)
 #pragma unroll
       for (int q = 0; q < D; ++q) Sig[p][q] = sc->Sig[p * D + q];
-    finalize_hyper<D, K>(sc->beta, Sig, a.omega2, a.hyper + (int64_t)c * HS);
+    finalize_hyper<D, K, false, !REPLAY && CLV_L2_NR != 0>(sc->beta, Sig, a.omega2, a.hyper + (int64_t)c * HS);
     CLV_STAMP(a.stamps, s, 7, false);
     if (store_l2) {
       int q = K * D;
@@ -2302,7 +2355,7 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
       for (int p = 0; p < D; ++p)
 #pragma unroll
         for (int q = 0; q < D; ++q) Sig[p][q] = l2.Sig[p * D + q];
-      finalize_hyper<D, K, true>(l2.beta, Sig, a.h.omega2, Hs);
+      finalize_hyper<D, K, true, CLV_L2_NR != 0>(l2.beta, Sig, a.h.omega2, Hs);
     }
     CLV_P_STAMP(a.stamps, wgi, 3, stp);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // resets landed (each wave its own)
