@@ -389,6 +389,18 @@ def run_leg(name: str, world: int, rank: int, local_rank: int, dist, steps: int,
             dt = float(t.item())
         return dt, kt
 
+    def run_clock():
+        """Average shader clock (GHz) of the last clv_run (clv_clock_ghz: s_memtime / s_memrealtime
+        at chain 0's level-2 publishes); at world size > 1 the ranks' min and max.  None if not
+        recorded.  Boxes of one pool run the same kernels at clocks ~13% apart."""
+        v = kern.clock_ghz()
+        if dist:
+            t = torch.tensor([v, -v], dtype=torch.float64, device=f"cuda:{local_rank}")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            lo, hi = -float(t[1].item()), float(t[0].item())
+            return dict(min=round(lo, 3), max=round(hi, 3)) if lo > 0 else None
+        return round(v, 3) if v > 0 else None
+
     def launch_roofline(first: int, n_t: int, kt, events_note: str):
         """Roofline of n_t sweeps starting at sweep `first` (persistent: kt of the timed launch)."""
         if kt is None:  # launch-per-sweep: event-timed pass over further sweeps of the same chains
@@ -431,6 +443,7 @@ def run_leg(name: str, world: int, rank: int, local_rank: int, dist, steps: int,
         run(warmup)
     sync()
     dt, kt = timed(steps, persistent)
+    clk = run_clock()  # the timed clv_run's average shader clock (outside the timed region)
     host_us = kern.host_times() if (host_split and persistent and not sharded) else None
     value = chains * n_total * steps / dt
     roof = launch_roofline(warmup + 1, steps if persistent else min(steps, timing_steps), kt,
@@ -452,7 +465,7 @@ def run_leg(name: str, world: int, rank: int, local_rank: int, dist, steps: int,
                      (f" ({kern.p2p_note})" if getattr(kern, "p2p_note", None) else "")),
                phase=f"burn-in (sweeps {warmup + 1}..{warmup + steps})" if phase == "burnin" else
                      f"stored (burn-in 0, sweeps {warmup + 1}..{warmup + steps})",
-               clock_settle_ms=round(settle_s * 1e3, 1))
+               clock_settle_ms=round(settle_s * 1e3, 1), gpu_clock_ghz=clk)
     if host_us:
         res["host_us"] = dict(host_us, clv_run_total=round(sum(host_us.values()), 3), timed_region=round(dt * 1e6, 3))
     if sharded:
@@ -481,6 +494,7 @@ def run_leg(name: str, world: int, rank: int, local_rank: int, dist, steps: int,
         sync()
         settle_clocks(settle_ms, local_rank)
         dt_st, kt_st = timed(steps, persistent)
+        clk_st = run_clock()
         first = burnin + 101
         n_st = steps if persistent else min(steps, timing_steps)
         roof_st = launch_roofline(first, n_st, kt_st, "the timed stored launch" if persistent else
@@ -495,7 +509,7 @@ def run_leg(name: str, world: int, rank: int, local_rank: int, dist, steps: int,
                              hbm_frac_kernel=round(bk * v_st / 1e9 / (world * HBM_PEAK_GBS), 5),
                              bytes_note="bytes_per_unit / hbm_frac: SURVEY §8d (summary sinks +0 per stored sweep); "
                                         "*_kernel: the kernel's own bytes incl. the running sums' read-modify-write",
-                             roofline=roof_st)
+                             roofline=roof_st, gpu_clock_ghz=clk_st)
         if WORKLOADS[name][1].startswith("synthetic:"):
             t_b, t_s = dt / steps, dt_st / steps
             res["whole_run"] = dict(value=chains * n_total * (burnin + mcmc_workload) / (burnin * t_b + mcmc_workload * t_s),
@@ -661,6 +675,10 @@ def main():
                         **({"phase": "stored (profiling: burn-in 0, every sweep stores)"} if a.phase == "stored" else {}),
                         timed_region=prim["_timed_region"]),
             clock_settle_ms=prim["clock_settle_ms"],
+            gpu_clock_ghz=prim.get("gpu_clock_ghz"),
+            gpu_clock_note="average shader clock of the timed clv_run (s_memtime / s_memrealtime between chain 0's "
+                           "level-2 publishes, clv_clock_ghz; persistent-kernel runs only, null for launch-per-sweep "
+                           "legs): boxes of one pool run the same cycles at clocks ~13% apart (DESIGN.md §8 round 5)",
             roofline=prim["roofline"], cpu_baseline=cpu,
             host_us=prim.get("host_us"),
             cold=prim.get("cold"),

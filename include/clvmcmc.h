@@ -152,6 +152,16 @@ int clv_partials(clv_sampler* s, double** device_ptr, int64_t* n_doubles, int32_
 int clv_copy_partials(clv_sampler* s, void* dst_device_ptr);
 int clv_synchronize(clv_sampler* s);
 int64_t clv_sweeps_done(const clv_sampler* s);
+
+/* Average shader clock (GHz) of the device over the last clv_run: s_memtime against s_memrealtime
+ * (100 MHz) over its sweeps but the last (at most the last 1024), each sweep's interval measured on
+ * one CU by chain 0's level-2 workgroup of the persistent kernel (s_memtime counts per XCD).  *ghz = 0
+ * when the run had fewer than 2 sweeps or ran without the persistent kernel (the launch-per-sweep
+ * kernel keeps no record: it measured 1-1.5% slower with one).  Measurement
+ * only — the reference has no counterpart; bench.py reports it beside every timed line, because
+ * MI355X boxes of one pool were measured to run the same cycles at clocks ~13% apart (DESIGN.md §8
+ * round 5).  Synchronizes the sampler's stream. */
+int clv_clock_ghz(clv_sampler* s, double* ghz);
 /* How clv_run launches: out[6] = (persistent 0/1, persistent-kernel workgroups per CU, CUs,
  * workgroups per sweep, reserved (0), reserved (0)).
  * Persistent = one launch for all of a clv_run's sweeps with every customer block resident, chosen

@@ -95,6 +95,7 @@ def lib() -> ctypes.CDLL:
         "clv_copy_partials": (c_int32, [sp, c_void_p]),
         "clv_synchronize": (c_int32, [sp]),
         "clv_sweeps_done": (c_int64, [sp]),
+        "clv_clock_ghz": (c_int32, [sp, POINTER(c_double)]),
         "clv_launch_info": (c_int32, [sp, POINTER(c_int64)]),
         "clv_p2p_info": (c_int32, [sp, POINTER(c_int64)]),
         "clv_p2p_export": (c_int32, [sp, c_void_p]),

@@ -79,6 +79,7 @@ SweepArgs sweep_args(clv_sampler* s, int init, int fuse = 0) {
   a.wait_ticks = s->wait_ticks;
   a.abort_host = s->d_h_abort;
   a.diag = s->d_diag;
+  a.clk = s->d_clk;
   a.h = hyper_args(s, nullptr, 0);
   if (fuse) a.h.hvar = s->replay ? nullptr : s->d_hvar;
   return a;
@@ -510,6 +511,8 @@ int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* pri
   CLV_HIPC(dalloc(&s->d_T, std::max<int64_t>(n, 1)));
   if (g.K > 1) CLV_HIPC(dalloc(&s->d_cov, (size_t)(g.K - 1) * std::max<int64_t>(n, 1)));
   if (g.D == 3) CLV_HIPC(dalloc(&s->d_logs, std::max<int64_t>(n, 1)));
+  CLV_HIPC(dalloc(&s->d_clk, 2 * CLK_RING));
+  CLV_HIPC(hipMemsetAsync(s->d_clk, 0, sizeof(unsigned long long) * 2 * CLK_RING, s->stream));
   CLV_HIPC(dalloc(&s->d_lam, C * std::max<int64_t>(n, 1)));
   CLV_HIPC(dalloc(&s->d_mu, C * std::max<int64_t>(n, 1)));
   CLV_HIPC(dalloc(&s->d_hyper, C * HS));
@@ -729,7 +732,8 @@ void clv_destroy(clv_sampler* s) {
   if (s->d_unit && s->d_unit != s->d_block) (void)hipFree(s->d_unit);
   if (s->d_hyp2) (void)hipFree(s->d_hyp2);
   for (void* p : {(void*)s->d_lam_alt, (void*)s->d_mu_alt, (void*)s->d_hyper_alt, (void*)s->d_sums_prev,
-                  (void*)s->d_pblock, (void*)s->d_qstore, (void*)s->d_pend, (void*)s->d_diag})
+                  (void*)s->d_pblock, (void*)s->d_qstore, (void*)s->d_pend, (void*)s->d_diag,
+                  (void*)s->d_clk})
     if (p) (void)hipFree(p);
   if (s->h_abort) (void)hipHostFree(s->h_abort);
   for (void* p : s->ipc_opened) (void)hipIpcCloseMemHandle(p);
@@ -825,6 +829,28 @@ int clv_synchronize(clv_sampler* s) {
 }
 
 int64_t clv_sweeps_done(const clv_sampler* s) { return s ? s->sweeps_done : -1; }
+
+int clv_clock_ghz(clv_sampler* s, double* ghz) {
+  if (!s || !ghz) return fail(CLV_EINVAL, "null argument");
+  *ghz = 0.0;
+  // the last clv_run's sweeps [first, end]: each slot is one workgroup's (delta s_memtime, delta
+  // s_memrealtime) up to that sweep's publish; the last sweep's draw may be deferred (persistent
+  // kernel), so it is left out; at most the last CLK_RING sweeps are kept
+  const int64_t end = s->sweeps_done - 1;
+  const int64_t first = std::max<int64_t>(s->clk_first, end - (CLK_RING - 1));
+  if (!s->d_clk || s->clk_first < 1 || end < first) return CLV_OK;
+  CLV_HIP(hipSetDevice(s->device));
+  CLV_HIP(hipStreamSynchronize(s->stream));
+  std::vector<unsigned long long> ring(2 * CLK_RING);
+  CLV_HIP(hipMemcpy(ring.data(), s->d_clk, sizeof(unsigned long long) * ring.size(), hipMemcpyDeviceToHost));
+  double dm = 0.0, dr = 0.0;
+  for (int64_t q = first; q <= end; ++q) {
+    dm += (double)ring[2 * (q % CLK_RING)];
+    dr += (double)ring[2 * (q % CLK_RING) + 1];
+  }
+  if (dr > 0.0) *ghz = 0.1 * dm / dr;  // s_memrealtime: 100 MHz
+  return CLV_OK;
+}
 
 int clv_launch_info(const clv_sampler* s, int64_t* out) {
   if (!s || !out) return fail(CLV_EINVAL, "null argument");
@@ -1194,6 +1220,7 @@ extern "C" {
 
 int clv_run(clv_sampler* s, int64_t n_sweeps) {
   if (!s) return fail(CLV_EINVAL, "null sampler");
+  s->clk_first = s->sweeps_done + 1;
   if (s->g.world_size != 1) {
     if (!s->p2p_ready) return fail(CLV_ESTATE, "sharded clv_run needs clv_p2p_connect; else use clv_sweep/clv_hyper");
     if (s->pending_init_hyper) return fail(CLV_ESTATE, "bivariate: call clv_hyper once before the first sweep");

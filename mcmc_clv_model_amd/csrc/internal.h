@@ -108,6 +108,8 @@ struct clv_sampler {
   uint32_t* h_abort = nullptr;      // host-mapped copy of ctrl->abort (the kernel stores it on a timeout)
   uint32_t* d_h_abort = nullptr;    // its device address
   unsigned long long* d_diag = nullptr;  // wait-timeout record (kernels.hip report_wait), DIAG_WORDS
+  unsigned long long* d_clk = nullptr;   // shader-clock record [CLK_RING][2] (SweepArgs::clk)
+  int64_t clk_first = 0;            // first sweep of the last clv_run (clv_clock_ghz)
   uint64_t wait_ticks = 0;          // bound on every persistent-kernel wait (s_memrealtime ticks)
   bool slots_dirty = true;          // persistent hand-off slots need the sentinel fill (a completed
                                     // launch leaves them empty; only an aborted one does not)

@@ -18,6 +18,7 @@ constexpr int HV = 40;                 // precomputed Philox hyper variates per 
                                        // chi2 [3,6), beta normals [8,35)
 constexpr int MAIL_TAIL = MAX_WORLD;   // peer mail: after the [2][world][chain][unit][stat] slots, one
                                        // progress word per rank (the sweep its level-2 side last polled for)
+constexpr int CLK_RING = 1024;         // shader-clock record (SweepArgs::clk): sweeps kept
 constexpr int DIAG_WORDS = 16;         // wait-timeout record (SweepArgs::diag, see kernels.hip report_wait)
 enum : int { WAIT_HYPER = 1, WAIT_BLOCKS = 2, WAIT_P2P_MAIL = 3, WAIT_FX_MAIL = 4 };
 
@@ -139,6 +140,10 @@ struct SweepArgs {
   // wait expires claims word 0 and writes what it was waiting for (kernels.hip report_wait); the
   // host formats it into clv_last_error()
   unsigned long long* diag;
+  // shader-clock record [CLK_RING][2] (device memory, or null): chain 0's level-2 side writes
+  // (s_memtime, s_memrealtime) when it publishes sweep s's draw, slot s % CLK_RING — clv_clock_ghz
+  // reads the run's first and last slots (the average clock the sweeps ran at)
+  unsigned long long* clk;
   HyperArgs h;               // level-2 arguments of the fused tail
   unsigned long long* stamps; // diagnostic build only (CLV_STAMPS): [1024][8] s_memrealtime stamps
 };

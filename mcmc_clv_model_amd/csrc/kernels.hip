@@ -1176,6 +1176,29 @@ __device__ __forceinline__ void post_progress(const SweepArgs& a, double* const*
                        __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// The shader clock against the 100 MHz s_memrealtime: (delta s_memtime, delta s_memrealtime) of one
+// interval of sweep s on one CU, chain 0 (SweepArgs::clk, clv_clock_ghz).
+// s_memtime counts per XCD — differences taken across CUs of different XCDs would be meaningless —
+// so each slot holds one workgroup's own interval: the persistent level-2 workgroup's from its
+// previous publish.  The launch-per-sweep kernel keeps no record: marks in one workgroup per launch
+// (its start to its block partial) measured c4 +1.5%, c5 +1% per sweep (profiles/r05_ab_clock_record.txt).
+#ifndef CLV_CLOCK_RECORD
+#define CLV_CLOCK_RECORD 1
+#endif
+struct ClockMark {
+  unsigned long long m, r;
+  __device__ __forceinline__ static ClockMark now() {
+    return ClockMark{__builtin_amdgcn_s_memtime(), __builtin_amdgcn_s_memrealtime()};
+  }
+};
+__device__ __forceinline__ ClockMark clock_mark(unsigned long long* clk, int64_t s, ClockMark from) {
+  const ClockMark t = ClockMark::now();
+  unsigned long long* p = clk + 2 * (s & (CLK_RING - 1));
+  p[0] = t.m - from.m;
+  p[1] = t.r - from.r;
+  return t;
+}
+
 // ---------------------------------------------------------------------------------------------
 // Sweep kernel
 // ---------------------------------------------------------------------------------------------
@@ -2108,6 +2131,7 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
   // being drawn from (the next launch's, or a flush's, iteration -1)
   const double* pin = P2P ? nullptr : a.pend_in;
   double* pout = P2P ? nullptr : a.pend_out;
+  ClockMark clk_prev = CLV_CLOCK_RECORD && a.clk && c == 0 ? ClockMark::now() : ClockMark{0, 0};  // per-sweep intervals
   for (int64_t it = pin ? -1 : 0; it < n_sweeps; ++it) {
     // the lane's addresses and unit bookkeeping are recomputed every sweep from an opaque copy of
     // the lane index (a few integer ops), not kept live across the loop: registers for the phases
@@ -2165,10 +2189,14 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
     if constexpr (P2P) {
       if (tid == 0) post_progress(a, s_peers, s);
     }
+    // one bound for the whole wait for sweep s's statistics, local partials and peer mail together,
+    // counted from its start: it then expires before the customer workgroups' wait for the (beta,
+    // Sigma) this draw would publish (which starts only after their partials), so the record names
+    // the missing peer unit rather than the slot that waited on it
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     {  // each wavefront polls on its own (no barrier per poll); a lane stops once its slots are full.
        // P2P: the mail is polled alongside (the other ranks' units of the last rank to finish are
        // then already in registers when its own partials are complete)
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       bool done = false;
       for (uint32_t poll = 0;; ++poll) {
         if (!done) {
@@ -2271,8 +2299,8 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
         for (int q = 0; q < g.world_size; ++q)
           if (q != a.rank) st_sys(s_peers[q] + dst + e, v);
       }
-      // 3c. the other ranks' units not seen yet
-      const uint64_t tw = __builtin_amdgcn_s_memrealtime();
+      // 3c. the other ranks' units not seen yet (the bound runs from t0, above)
+      const uint64_t tw = t0;
       for (uint32_t poll = 0; !__all(mdone); ++poll) {
         if (!mdone) {
           bool ok = true;
@@ -2368,6 +2396,7 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
     }
     CLV_P_STAMP(a.stamps, wgi, 4, stp);
     CLV_P_STAMP(a.stamps, wgi, 5, tid == 0 && it + 1 == it_stamp);  // the previous sweep's publish
+    if (CLV_CLOCK_RECORD && a.clk && c == 0 && tid == 0) clk_prev = clock_mark(a.clk, s, clk_prev);
 #ifdef CLV_STAMPS
     if (tid == 0 && a.stamps && c < 8 && it % 4 == 0 && it / 4 < 1024)  // publish times, every 4th sweep
       a.stamps[(it / 4) * 8 + c] = __builtin_amdgcn_s_memrealtime();

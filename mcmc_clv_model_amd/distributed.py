@@ -346,6 +346,11 @@ class ShardedSampler:
         info["persistent"] = self.exchange == "p2p" and self.s.p2p_info()["persistent"]
         return info
 
+    def clock_ghz(self) -> float:
+        """This rank's average shader clock over its last clv_run (p2p / fused exchange); 0.0 on the
+        RCCL path, which runs clv_sweep / clv_hyper and keeps no record."""
+        return self.s.clock_ghz() if self.exchange == "p2p" else 0.0
+
     def set_timing(self, enable: bool) -> None:
         self.timing = bool(enable)
         self.s.set_timing(enable)

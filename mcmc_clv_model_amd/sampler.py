@@ -249,6 +249,13 @@ class HipSampler:
         names = ("set_device", "start_event", "launch_call", "end_event", "wait", "return")
         return {k: round(h[i + 1] - h[i], 3) for i, k in enumerate(names)}
 
+    def clock_ghz(self) -> float:
+        """clv_clock_ghz: the average shader clock (GHz) over the last run() (0.0 when not recorded:
+        fewer than 3 sweeps, or the RCCL-sharded path)."""
+        v = ctypes.c_double(0.0)
+        check(self._L.clv_clock_ghz(self.h, ctypes.byref(v)))
+        return float(v.value)
+
     def launch_info(self) -> dict:
         """How clv_run launches (clv_launch_info): persistent kernel or one launch per sweep."""
         out = (ctypes.c_int64 * 6)()

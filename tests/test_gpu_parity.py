@@ -304,6 +304,31 @@ def test_stream_draws_arguments(L):
         assert np.array_equal(bits(d["level_1"][c]), bits(l1[c])) and np.array_equal(bits(d["level_2"][c]), bits(l2[c]))
 
 
+def test_clock_record_persistent_and_launch_per_sweep(L):
+    """clv_clock_ghz: the shader clock over a run of the persistent kernel, from chain 0's level-2
+    workgroup's (s_memtime, s_memrealtime) between publishes (per-CU intervals: s_memtime counts per
+    XCD); 0 for a one-sweep run and for the launch-per-sweep kernel, which keeps no record.  MI355X's
+    engine clock is at most 2.4 GHz."""
+    from mcmc_clv_model_amd.sampler import HipSampler, build_problem
+    from mcmc_clv_model_amd.data import synthetic_cbs
+    cases = [(build_problem(cdnow("full"), ["first_sales_scaled"], 2), 4, True),
+             (build_problem(synthetic_cbs(150_000, 5, seed=3), [f"c{k}" for k in range(1, 5)], 2), 2, False)]
+    for p, chains, persistent in cases:
+        with HipSampler(p, mcmc=1000, burnin=1000, thin=10, chains=chains, seed=9, draw_sink="summary") as s:
+            assert s.launch_info()["persistent"] == persistent
+            s.run(1)
+            assert s.clock_ghz() == 0.0
+            s.run(200)
+            ghz = s.clock_ghz()
+            print(f"persistent={persistent}: {ghz:.3f} GHz")
+            if not persistent:
+                assert ghz == 0.0
+                continue
+            assert 0.5 < ghz < 2.6
+            s.run(1500)  # longer than the record (the last 1024 sweeps)
+            assert 0.5 < s.clock_ghz() < 2.6
+
+
 @pytest.mark.parametrize("val", ["inf", "nan", "0x10", "5 ms"])
 def test_wait_timeout_env_rejected(L, monkeypatch, val):
     """a CLV_WAIT_TIMEOUT_MS that is not a finite decimal number fails clv_create (EINVAL)

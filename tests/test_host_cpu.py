@@ -579,6 +579,9 @@ def test_bench_config_times_the_stored_phase(monkeypatch):
             n = sum(b - a + 1 for a, b, t in log if t)
             return dict(sweep_ms=0.085 * n, sweep_launches=n, hyper_ms=0.0, hyper_launches=0)
 
+        def clock_ghz(self):
+            return 2.25
+
         def close(self):
             pass
 
@@ -602,6 +605,7 @@ def test_bench_config_times_the_stored_phase(monkeypatch):
     assert abs(roof["launch_us"] - 85.0) < 1e-6 and roof["sweeps_per_launch"] == 1
     assert abs(roof["achieved"] - 84.0 * 500 / 85e-6 / 1e9) < 1e-3
     assert r["stored"]["roofline"]["bound"] is not None
+    assert r["gpu_clock_ghz"] == 2.25 and r["stored"]["gpu_clock_ghz"] == 2.25  # clv_clock_ghz of the timed runs
     tb, ts = r["ms_per_step"], r["stored"]["ms_per_step"]
     n = 500
     want = n * 10000 / (5000 * tb + 5000 * ts) * 1e3
