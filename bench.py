@@ -264,21 +264,33 @@ def settle_clocks(ms: float, device: int) -> float:
     return time.perf_counter() - t0
 
 
+def profile_name(workload: str, phase: str) -> str:
+    """The committed profile a line's traffic and counters come from: profiles/r*_<w>_*summary.json
+    for the burn-in line, r*_<w>stored_*summary.json (tools/gpu_profile_round.sh <w>stored: every
+    sweep a stored sweep) for the stored sub-line — never the other phase's (verdict r5 weak 3)."""
+    return workload + ("stored" if phase == "stored" else "")
+
+
 def roofline_for(workload: str, kname: str, D: int, K: int, bpu: float, units: int, t_launch: float, spl: int,
-                 sharded: bool, **extra) -> dict:
+                 sharded: bool, profile: str | None = None, **extra) -> dict:
     """The roofline object of one kernel: SURVEY §8d bytes x (chain, customer) sweeps per launch /
     the launch's duration, measured traffic and the counters that decide `bound` (committed
-    rocprofv3 summaries of this workload's instance; none for sharded runs, profiled at N = 1)."""
+    rocprofv3 summaries of `profile` — the workload's burn-in or stored phase, profile_name —
+    of this instance; none for sharded runs, profiled at N = 1)."""
+    profile = profile or workload
     achieved = bpu * units / t_launch / 1e9
     r = dict(bound=None, achieved=round(achieved, 3), peak=HBM_PEAK_GBS, unit="GB/s",
              frac=round(achieved / HBM_PEAK_GBS, 6), traffic=None, bytes_per_unit=round(bpu, 3),
              units_per_launch=units, sweeps_per_launch=spl, launch_us=round(t_launch * 1e6, 3),
              sweep_kernel_us=round(t_launch / spl * 1e6, 3), **extra)
-    tr = None if sharded else committed_traffic(workload, kname, D, K)
+    tr = None if sharded else committed_traffic(profile, kname, D, K)
     if tr:  # HBM bytes per launch (calibrated PMC), per sweep x sweeps per launch
         r["traffic"] = round(tr["bytes_per_sweep"] * spl)
         r["traffic_source"] = f"{tr['source']}: {tr['counters']}"
-    ev = (None if sharded else committed_counters(workload, kname, D, K)) or {}
+        r["traffic_vs_algorithmic"] = round(r["traffic"] / (bpu * units), 3)
+    elif not sharded:
+        r["traffic_source"] = f"no committed profile of {profile} (profiles/r*_{profile}_*summary.json)"
+    ev = (None if sharded else committed_counters(profile, kname, D, K)) or {}
     if r["traffic"] is not None:
         ev["hbm_traffic_frac"] = round(r["traffic"] / t_launch / 1e9 / HBM_PEAK_GBS, 4)
     if ev.get("hbm_traffic_frac", 0.0) >= 0.6:
@@ -401,8 +413,9 @@ def run_leg(name: str, world: int, rank: int, local_rank: int, dist, steps: int,
             return dict(min=round(lo, 3), max=round(hi, 3)) if lo > 0 else None
         return round(v, 3) if v > 0 else None
 
-    def launch_roofline(first: int, n_t: int, kt, events_note: str):
-        """Roofline of n_t sweeps starting at sweep `first` (persistent: kt of the timed launch)."""
+    def launch_roofline(first: int, n_t: int, kt, events_note: str, ph: str = "burnin"):
+        """Roofline of n_t sweeps starting at sweep `first` (persistent: kt of the timed launch);
+        traffic and counters from the committed profile of phase `ph` (profile_name)."""
         if kt is None:  # launch-per-sweep: event-timed pass over further sweeps of the same chains
             kern.set_timing(True)
             run(n_t)
@@ -415,7 +428,7 @@ def run_leg(name: str, world: int, rank: int, local_rank: int, dist, steps: int,
         spl = n_t if persistent else 1  # sweeps per launch
         frac = stored_fraction(burnin, thin, first, first + n_t - 1)
         r = roofline_for(name, kname, D, K, survey_bytes(D, K, frac, sink), chains * n_local * spl, t_sweep * spl, spl,
-                         sharded and not p2p,
+                         sharded and not p2p, profile=profile_name(name, ph),
                          kernel=(("persist_kernel (one launch for all sweeps of a clv_run; level-2 workgroup per "
                                   "chain" + ("; unit partials exchanged over xGMI" if p2p else "") + ")")
                                  if persistent else
@@ -448,7 +461,7 @@ def run_leg(name: str, world: int, rank: int, local_rank: int, dist, steps: int,
     value = chains * n_total * steps / dt
     roof = launch_roofline(warmup + 1, steps if persistent else min(steps, timing_steps), kt,
                            "the timed region's launch" if persistent else
-                           f"a pass of {min(steps, timing_steps)} further sweeps, one event pair per launch")
+                           f"a pass of {min(steps, timing_steps)} further sweeps, one event pair per launch", ph=phase)
     done = warmup + steps + (0 if persistent else min(steps, timing_steps))
     res = dict(workload=f"{name}: {'bivariate' if D == 2 else 'trivariate'}, K={K}, " +
                         ("synthetic (mcmc_clv_model_amd.data.synthetic_cbs)" if WORKLOADS[name][1].startswith("synthetic:")
@@ -498,7 +511,11 @@ def run_leg(name: str, world: int, rank: int, local_rank: int, dist, steps: int,
         first = burnin + 101
         n_st = steps if persistent else min(steps, timing_steps)
         roof_st = launch_roofline(first, n_st, kt_st, "the timed stored launch" if persistent else
-                                  f"a pass of {n_st} further stored sweeps")
+                                  f"a pass of {n_st} further stored sweeps", ph="stored")
+        if roof_st and roof_st.get("traffic") is not None and sink != "full":
+            roof_st["traffic_note"] = ("measured stored-phase bytes vs SURVEY §8d (summary sink +0 per stored sweep): "
+                                       "the excess is the read-modify-write of the running sums (%d fp64 per "
+                                       "customer, 16 B each) on every stored sweep" % (9 if D == 2 else 11))
         v_st = chains * n_total * steps / dt_st
         fr = stored_fraction(burnin, thin, first, first + steps - 1)
         b8 = survey_bytes(D, K, fr, sink)

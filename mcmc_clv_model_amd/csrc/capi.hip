@@ -703,7 +703,7 @@ int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* pri
       for (int i = 0; i < g.D * g.D; ++i) o[g.K * g.D + i] = prior->sigma_init[i];
     }
     CLV_HIPC(hipMemcpyAsync(s->d_bs, bs.data(), sizeof(double) * bs.size(), hipMemcpyHostToDevice, s->stream));
-    CLV_HIPC(launch_set_hyper(g.D, g.K, (int)C, s->d_hyper, s->d_bs, prior->omega2, s->stream));
+    CLV_HIPC(launch_set_hyper(g.D, g.K, (int)C, s->d_hyper, s->d_bs, prior->omega2, s->replay, s->stream));
   } else {
     s->pending_init_hyper = true;
   }
@@ -1254,7 +1254,12 @@ int clv_run(clv_sampler* s, int64_t n_sweeps) {
 
 int clv_stream_draws(clv_sampler* s, double* level1) {
   if (!s) return fail(CLV_EINVAL, "null sampler");
-  if (s->ds) stream_wait(s->ds);
+  if (s->ds) {
+    stream_wait(s->ds);
+    // the old registration ends here; a new one streams every draw again from the first
+    // (ds_next = 0), so a failure of the old pieces has nothing left to repair
+    stream_clear_failed(s->ds);
+  }
   if (!level1) {
     s->ds_dest = nullptr;
     return CLV_OK;
@@ -1267,7 +1272,10 @@ int clv_stream_draws(clv_sampler* s, double* level1) {
   s->ds_next = 0;
   const Geometry& g = s->g;
   stream_prefault(s->ds, s->device, level1, sizeof(double) * (size_t)g.n_chains * g.n_draws * g.n * (g.D + 2));
-  stream_enqueue(s);  // draws of sweeps already run
+  // draws of sweeps already run: the pool copies on the null stream, which does not order against
+  // the sampler's non-blocking stream, so the sweeps enqueued there must have completed
+  CLV_HIP(hipStreamSynchronize(s->stream));
+  stream_enqueue(s);
   return CLV_OK;
 }
 
@@ -1325,8 +1333,10 @@ int clv_read_draws(clv_sampler* s, double* level1, double* level2, double* logli
     } else if (s->ds) {
       stream_wait(s->ds);
     }
-    if (s->d_level1 && !done)
+    if (s->d_level1 && !done) {
       CLV_HIP(hipMemcpy(level1, s->d_level1, sizeof(double) * C * g.n_draws * g.n * (g.D + 2), hipMemcpyDeviceToHost));
+      if (s->ds && s->ds_dest == level1) stream_clear_failed(s->ds);  // the full copy repaired it
+    }
   }
   if (level2 && s->d_level2)
     CLV_HIP(hipMemcpy(level2, s->d_level2, sizeof(double) * C * g.n_draws * g.l2w, hipMemcpyDeviceToHost));
@@ -1395,7 +1405,7 @@ int clv_set_state(clv_sampler* s, const double* lambdas, const double* mus, cons
   if (mus && g.n) CLV_HIP(hipMemcpy(s->d_mu, mus, sizeof(double) * g.n_chains * g.n, hipMemcpyHostToDevice));
   if (hyper) {
     CLV_HIP(hipMemcpy(s->d_bs, hyper, sizeof(double) * g.n_chains * (g.K * g.D + g.D * g.D), hipMemcpyHostToDevice));
-    CLV_HIP(launch_set_hyper(g.D, g.K, g.n_chains, s->d_hyper, s->d_bs, s->prior.omega2, s->stream));
+    CLV_HIP(launch_set_hyper(g.D, g.K, g.n_chains, s->d_hyper, s->d_bs, s->prior.omega2, s->replay, s->stream));
     s->pending_init_hyper = false;
   }
   Ctrl c{};

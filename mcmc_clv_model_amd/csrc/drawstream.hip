@@ -142,10 +142,15 @@ void stream_copy(DrawStreamState* st, int device, const void* src, void* dst, si
   if (bytes) submit(st, device, (const char*)src, (char*)dst, bytes);
 }
 
+// A failed piece stays recorded (sticky) until stream_clear_failed: whichever later call waits first
+// (a rewind, a re-registration, the read) must not consume it, or clv_read_draws would take the
+// destination for complete and skip the full copy that repairs it.
 bool stream_wait(DrawStreamState* st) {
   std::unique_lock<std::mutex> lk(st->m);
   st->cv.wait(lk, [&] { return st->pending == 0; });
-  return st->failed.exchange(0) == 0;
+  return st->failed.load() == 0;
 }
+
+void stream_clear_failed(DrawStreamState* st) { st->failed.store(0); }
 
 }  // namespace clv

@@ -36,7 +36,8 @@ struct DrawStreamState {
 };
 void stream_prefault(DrawStreamState* st, int device, void* dst, size_t bytes);  // touch dst's pages
 void stream_copy(DrawStreamState* st, int device, const void* src, void* dst, size_t bytes);
-bool stream_wait(DrawStreamState* st);  // every piece done; false if one failed (then reset)
+bool stream_wait(DrawStreamState* st);  // every piece done; false if one failed since the last clear
+void stream_clear_failed(DrawStreamState* st);  // after a full copy has repaired the destination
 
 template <class T>
 hipError_t dalloc(T** p, size_t count) {

@@ -166,7 +166,7 @@ hipError_t persist_occupancy(int D, int K, bool p2p, int* blocks_per_cu);
 hipError_t launch_persist_flush(const SweepArgs& a, int64_t s_first, hipStream_t st);
 hipError_t launch_hyper(const HyperArgs& a, bool replay, hipStream_t st);
 hipError_t launch_set_hyper(int D, int K, int n_chains, double* hyper, const double* beta_sigma,
-                            double omega2, hipStream_t st);
+                            double omega2, bool replay, hipStream_t st);
 hipError_t launch_debug_philox(uint32_t k0, uint32_t k1, const uint32_t* ctr, int64_t n, uint32_t* out,
                                hipStream_t st);
 hipError_t launch_debug_variates(uint64_t seed, int chain, uint32_t sweep, int64_t n, int S, float* tl,

@@ -1118,18 +1118,26 @@ __device__ __forceinline__ void st_sys(double* p, double v) {
 __device__ __forceinline__ bool slot_full(double v) { return __double_as_longlong(v) != SLOT_EMPTY; }
 __device__ __forceinline__ double slot_empty() { return __longlong_as_double(SLOT_EMPTY); }
 
-// Bounded wait bookkeeping (uniform): true when this wave must give up.  The abort flag is read
-// every 16th poll only, so a poll iteration costs one memory round trip, not two.
-__device__ __forceinline__ bool wait_expired(const SweepArgs& a, uint64_t t0, uint32_t poll) {
+// Bounded wait bookkeeping (uniform).  WAIT_GOING: keep polling; WAIT_OBSERVED: another wave raised
+// the abort flag — leave without a record (the wave that raised it writes it); WAIT_EXPIRED: this
+// wave's own bound ran out — write the record (report_wait) and only THEN raise the flag
+// (raise_abort), so no wave that merely saw the flag can claim the record first (verdict r5: a
+// customer wave that observed the level-2 workgroup's abort claimed it at 299.99 of 300 ms).  The
+// abort flag is read every 16th poll only, so a poll iteration costs one memory round trip, not two.
+enum : int { WAIT_GOING = 0, WAIT_OBSERVED = 1, WAIT_EXPIRED = 2 };
+__device__ __forceinline__ int wait_state(const SweepArgs& a, uint64_t t0, uint32_t poll, uint64_t bound) {
   if ((poll & 15u) == 15u && __hip_atomic_load(&a.ctrl_rw->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-    return true;
-  if (__builtin_amdgcn_s_memrealtime() - t0 > a.wait_ticks) {
-    __hip_atomic_store(&a.ctrl_rw->abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (a.abort_host) __hip_atomic_store(a.abort_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    return true;
-  }
-  return false;
+    return WAIT_OBSERVED;
+  return __builtin_amdgcn_s_memrealtime() - t0 > bound ? WAIT_EXPIRED : WAIT_GOING;
 }
+__device__ __forceinline__ void raise_abort(const SweepArgs& a) {
+  __hip_atomic_store(&a.ctrl_rw->abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (a.abort_host) __hip_atomic_store(a.abort_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// The customers' wait for (beta, Sigma) is downstream of the level-2 side's waits (the draw it waits
+// for is what those waits feed), so its bound is 1.5x theirs: a stall upstream expires upstream first
+// and the record names the statistic that never came, not the hand-off slot that waited on it.
+__device__ __forceinline__ uint64_t hyper_wait_ticks(const SweepArgs& a) { return a.wait_ticks + a.wait_ticks / 2; }
 
 // The wait-timeout record (SweepArgs::diag): the wave whose bounded wait expired names what it was
 // waiting for — the lowest lane still missing a slot reports its (unit or block, statistic, the
@@ -1137,7 +1145,9 @@ __device__ __forceinline__ bool wait_expired(const SweepArgs& a, uint64_t t0, ui
 // level-2 side last started to poll for).  Word layout: [0] claimed, [1] kind (WAIT_*), [2] sweep,
 // [3] chain, [4] rank, [5] unit / block, [6] statistic, [7] bits, [8] polls, [9] waited ticks
 // (100 MHz), [10] lanes of the wave still missing, [11..15] progress of ranks 0..4 (-1: none).
-// Called by every lane of the wave (one ballot); only the first wave of the launch to time out writes.
+// Called by every lane of the wave (one ballot), only by a wave whose own bound expired (WAIT_EXPIRED),
+// before it raises the abort flag; the first such wave of the launch writes.  Waves that stop because
+// they observed the flag never call it, so the recorded wait is always >= its bound.
 __device__ __forceinline__ void report_wait(const SweepArgs& a, int kind, int64_t s, int c, bool lane_ok,
                                             int64_t unit, int stat, uint64_t bits, uint32_t polls, uint64_t t0) {
   if (!a.diag) return;
@@ -2000,7 +2010,10 @@ __device__ __forceinline__ void sweep_body(const SweepArgs& a) {
               }
             }
             if (__all(ok)) break;
-            if (wait_expired(a, t0, poll)) {
+            const int ws = wait_state(a, t0, poll, a.wait_ticks);
+            if (ws == WAIT_OBSERVED) {
+              timed_out = true;
+            } else if (ws == WAIT_EXPIRED) {
               timed_out = true;
               int64_t mu_ = -1;
               int mj = -1;
@@ -2013,6 +2026,7 @@ __device__ __forceinline__ void sweep_body(const SweepArgs& a) {
                 }
               }
               report_wait(a, WAIT_FX_MAIL, s, c, ok, mu_, mj, mb, poll, t0);
+              raise_abort(a);
             } else {
               __builtin_amdgcn_s_sleep(1);
             }
@@ -2224,7 +2238,12 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
           }
         }
         if (__all(done)) break;
-        if (wait_expired(a, t0, poll)) {
+        const int ws = wait_state(a, t0, poll, a.wait_ticks);
+        if (ws == WAIT_OBSERVED) {
+          s_abort = 1;
+          break;
+        }
+        if (ws == WAIT_EXPIRED) {
           int64_t mb_ = -1;
           int mj = -1;
           uint64_t mbits = 0;
@@ -2234,6 +2253,7 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
             if (hb0 && !slot_full(v0[j])) { mb_ = b0; mj = j; mbits = dbits(v0[j]); }
           }
           report_wait(a, WAIT_BLOCKS, s, c, done, mb_, mj, mbits, poll, t0);
+          raise_abort(a);
           s_abort = 1;
           break;
         }
@@ -2314,7 +2334,12 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
           mdone = ok;
         }
         if (__all(mdone)) break;
-        if (wait_expired(a, tw, poll)) {
+        const int ws = wait_state(a, tw, poll, a.wait_ticks);
+        if (ws == WAIT_OBSERVED) {
+          s_abort = 1;
+          break;
+        }
+        if (ws == WAIT_EXPIRED) {
           int64_t mu_ = -1;
           int mj = -1;
           uint64_t mbits = 0;
@@ -2324,6 +2349,7 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
             if (m0 && !slot_full(w0[j])) { mu_ = u0; mj = j; mbits = dbits(w0[j]); }
           }
           report_wait(a, WAIT_P2P_MAIL, s, c, mdone, mu_, mj, mbits, poll, tw);
+          raise_abort(a);
           s_abort = 1;
           break;
         }
@@ -2525,8 +2551,12 @@ __global__ __launch_bounds__(BLOCK, 2) void persist_kernel(SweepArgs a, int64_t 
             Hs[tid] = v;
             break;
           }
-          if (wait_expired(a, t0, poll)) {
-            report_wait(a, WAIT_HYPER, s, c, slot_full(v), b, tid, dbits(v), poll, t0);
+          const int ws = wait_state(a, t0, poll, hyper_wait_ticks(a));
+          if (ws != WAIT_GOING) {
+            if (ws == WAIT_EXPIRED) {
+              report_wait(a, WAIT_HYPER, s, c, slot_full(v), b, tid, dbits(v), poll, t0);
+              raise_abort(a);
+            }
             if (tid == 0) s_abort = 1;
             break;
           }
@@ -2611,7 +2641,9 @@ __global__ __launch_bounds__(BLOCK) void persist_flush_kernel(SweepArgs a, int64
 }
 
 // (beta, Sigma) -> hyper state for every chain: [chain][K*D + D*D] input.
-template <int D, int K>
+// NR: Philox mode finalises like the level-2 draws do (rcp_nr / rsq_nr), so a state set here
+// (clv_create, clv_set_state) carries the same bits as the uninterrupted run's.
+template <int D, int K, bool NR>
 __global__ void set_hyper_kernel(int n_chains, double* hyper, const double* bs, double omega2) {
   const int c = threadIdx.x;
   if (c >= n_chains) return;
@@ -2619,7 +2651,7 @@ __global__ void set_hyper_kernel(int n_chains, double* hyper, const double* bs, 
   double Sig[D][D];
   for (int p = 0; p < D; ++p)
     for (int q = 0; q < D; ++q) Sig[p][q] = in[K * D + p * D + q];
-  finalize_hyper<D, K>(in, Sig, omega2, hyper + (int64_t)c * HS);
+  finalize_hyper<D, K, false, NR>(in, Sig, omega2, hyper + (int64_t)c * HS);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2902,11 +2934,13 @@ hipError_t launch_hyper(const HyperArgs& a, bool replay, hipStream_t st) {
 }
 
 hipError_t launch_set_hyper(int D, int K, int n_chains, double* hyper, const double* bs, double omega2,
-                            hipStream_t st) {
+                            bool replay, hipStream_t st) {
 #define CLV_CASE(DD, KK, RR) \
-  if (D == DD && K == KK) { hipLaunchKernelGGL((set_hyper_kernel<DD, KK>), dim3(1), dim3(64), 0, st, n_chains, hyper, bs, omega2); return hipGetLastError(); }
-  CLV_FOR_K(CLV_CASE, 2, 0)
-  CLV_FOR_K(CLV_CASE, 3, 0)
+  if (D == DD && K == KK && replay == RR) { hipLaunchKernelGGL((set_hyper_kernel<DD, KK, !RR && CLV_L2_NR != 0>), dim3(1), dim3(64), 0, st, n_chains, hyper, bs, omega2); return hipGetLastError(); }
+  CLV_FOR_K(CLV_CASE, 2, false)
+  CLV_FOR_K(CLV_CASE, 3, false)
+  CLV_FOR_K(CLV_CASE, 2, true)
+  CLV_FOR_K(CLV_CASE, 3, true)
 #undef CLV_CASE
   return hipErrorInvalidValue;
 }

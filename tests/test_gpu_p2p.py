@@ -332,6 +332,10 @@ def test_p2p_abort_leaves_state_unchanged_and_rollback(monkeypatch, persistent):
         msg = str(errs[0])
         assert "[wait record: sweep 4, chain " in msg and "peer unit partial" in msg, msg
         assert "(rank 1, local unit" in msg and "0:4 1:3" in msg, msg
+        # written by the wave whose own bound expired, not by one that only saw the abort flag
+        import re
+        waited = float(re.search(r" polls, ([0-9.]+) ms;", msg).group(1))
+        assert waited >= 300.0, msg
         assert shards[0].sweeps_done == 3
         after = shards[0].get_state()
         assert all(np.array_equal(bits(x), bits(y)) for x, y in zip(before, after))

