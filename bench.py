@@ -46,6 +46,9 @@ WORKLOADS = {
     # synthetic: 1M customers K=5 bivariate; 1.25M customers per GPU K=9 trivariate
     "c4": (2, "synthetic:1000000:5:20250718", ["c1", "c2", "c3", "c4"], 1, 5000, 5000, 1, "summary"),
     "c5": (3, "synthetic:1250000:9:20250719", [f"c{k}" for k in range(1, 9)], 1, 5000, 5000, 1, "summary"),
+    # NOT a BASELINE configuration: the instance one GPU runs in c4's 8-rank run — rank 0's shard of
+    # distributed.plan(1M, 8), 496 blocks = 126,976 customers of the c4 set (verdict r5 #4), at world size 1
+    "c4_shard8": (2, "synthetic:1000000:5:20250718:shard0of8", ["c1", "c2", "c3", "c4"], 1, 5000, 5000, 1, "summary"),
 }
 BASELINE_INDEX = {"c1": 0, "c2": 1, "c3": 2, "c4": 3, "c5": 4}
 
@@ -60,8 +63,8 @@ def config_legs(world: int, primary: str):
     """The `configs` legs: every other BASELINE configuration at this N (c1 and c3 are one-GPU
     configurations; at N > 1 c2 runs tiled once per rank, a non-BASELINE rehearsal of the
     CDNOW-size exchange)."""
-    if world == 1:
-        return [c for c in ("c3", "c4", "c5") if c != primary]
+    if world == 1:  # (+ c4_shard8: the per-GPU instance of c4's 8-rank run, a single-GPU proxy)
+        return [c for c in ("c3", "c4", "c5", "c4_shard8") if c != primary]
     return [c for c in ("c4", "c2") if c != primary]
 
 
@@ -101,6 +104,7 @@ def _kernel_matches(name: str, kname: str, D: int, K: int) -> bool:
 def _summaries(workload: str):
     import glob
     out = []
+    workload = workload.replace("_", "")  # profile names carry no "_" inside the workload (profile_name)
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{workload}_*summary.json"))):
         try:
             out.append((path, json.load(open(path))))
@@ -163,9 +167,14 @@ def load_workload(name: str, world: int = 1):
     from mcmc_clv_model_amd.data import add_driver_columns, synthetic_cbs
     D, data, covs, chains, burnin, mcmc, thin, sink = WORKLOADS[name]
     if data.startswith("synthetic:"):
-        _, n, K, seed = data.split(":")
+        _, n, K, seed, *shard = data.split(":")
         n = int(n) * (world if name == "c5" else 1)
         df = synthetic_cbs(n, int(K), D, seed=int(seed))
+        if shard:  # "shard<r>of<w>": rank r's customers of distributed.plan(n, w)
+            from mcmc_clv_model_amd.distributed import plan
+            r, w = (int(v) for v in shard[0][len("shard"):].split("of"))
+            b, e = plan(n, w).shard(r)
+            df = df.iloc[b:e].reset_index(drop=True)
     else:
         d = np.load(os.path.join(ROOT, "tests", "golden", f"cdnow_{data}_cbs.npz"), allow_pickle=False)
         df = add_driver_columns(pd.DataFrame({k: d[k] for k in d.files}))
@@ -268,7 +277,7 @@ def profile_name(workload: str, phase: str) -> str:
     """The committed profile a line's traffic and counters come from: profiles/r*_<w>_*summary.json
     for the burn-in line, r*_<w>stored_*summary.json (tools/gpu_profile_round.sh <w>stored: every
     sweep a stored sweep) for the stored sub-line — never the other phase's (verdict r5 weak 3)."""
-    return workload + ("stored" if phase == "stored" else "")
+    return workload.replace("_", "") + ("stored" if phase == "stored" else "")  # c4_shard8 -> c4shard8
 
 
 def roofline_for(workload: str, kname: str, D: int, K: int, bpu: float, units: int, t_launch: float, spl: int,
@@ -402,16 +411,22 @@ def run_leg(name: str, world: int, rank: int, local_rank: int, dist, steps: int,
         return dt, kt
 
     def run_clock():
-        """Average shader clock (GHz) of the last clv_run (clv_clock_ghz: s_memtime / s_memrealtime
-        at chain 0's level-2 publishes); at world size > 1 the ranks' min and max.  None if not
-        recorded.  Boxes of one pool run the same kernels at clocks ~13% apart."""
-        v = kern.clock_ghz()
+        """Shader clock (GHz) the timed launches ran at: the persistent kernel's own record of the
+        last clv_run (clv_clock_ghz: s_memtime / s_memrealtime at chain 0's level-2 publishes), else
+        a 50 us probe kernel enqueued right behind them (clv_clock_probe; the launch-per-sweep kernel
+        keeps no record).  Returns (clock, source, probe); at world size > 1 the clock is the ranks'
+        min and max.  Boxes of one pool run the same kernels at clocks ~13% apart."""
+        rec = kern.clock_ghz()
+        probe = kern.clock_probe(50.0)
+        v = rec if rec > 0 else probe
+        src = "clv_clock_ghz (in-kernel record)" if rec > 0 else ("clv_clock_probe (50 us probe kernel behind "
+                                                                  "the timed launches)" if v > 0 else None)
         if dist:
             t = torch.tensor([v, -v], dtype=torch.float64, device=f"cuda:{local_rank}")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             lo, hi = -float(t[1].item()), float(t[0].item())
-            return dict(min=round(lo, 3), max=round(hi, 3)) if lo > 0 else None
-        return round(v, 3) if v > 0 else None
+            return (dict(min=round(lo, 3), max=round(hi, 3)) if lo > 0 else None), src, round(probe, 3)
+        return (round(v, 3) if v > 0 else None), src, (round(probe, 3) if probe > 0 else None)
 
     def launch_roofline(first: int, n_t: int, kt, events_note: str, ph: str = "burnin"):
         """Roofline of n_t sweeps starting at sweep `first` (persistent: kt of the timed launch);
@@ -456,7 +471,7 @@ def run_leg(name: str, world: int, rank: int, local_rank: int, dist, steps: int,
         run(warmup)
     sync()
     dt, kt = timed(steps, persistent)
-    clk = run_clock()  # the timed clv_run's average shader clock (outside the timed region)
+    clk, clk_src, clk_probe = run_clock()  # the timed launches' shader clock (outside the timed region)
     host_us = kern.host_times() if (host_split and persistent and not sharded) else None
     value = chains * n_total * steps / dt
     roof = launch_roofline(warmup + 1, steps if persistent else min(steps, timing_steps), kt,
@@ -466,8 +481,9 @@ def run_leg(name: str, world: int, rank: int, local_rank: int, dist, steps: int,
     res = dict(workload=f"{name}: {'bivariate' if D == 2 else 'trivariate'}, K={K}, " +
                         ("synthetic (mcmc_clv_model_amd.data.synthetic_cbs)" if WORKLOADS[name][1].startswith("synthetic:")
                          else f"CDNOW {WORKLOADS[name][1]} CBS"),
-               baseline_config=BASELINE_INDEX[name],
-               scaling="strong" if name == "c4" else "weak", value=value, unit="customer-sweeps/s",
+               baseline_config=BASELINE_INDEX.get(name),
+               scaling="strong" if name == "c4" else "proxy" if name == "c4_shard8" else "weak", value=value,
+               unit="customer-sweeps/s",
                n_customers=n_total, customers_per_gpu=n_total // world, chains=chains, steps=steps, warmup=warmup,
                ms_per_step=dt / steps * 1e3, draw_sink=sink, burnin=burnin, mcmc=mcmc_workload, thin=thin,
                roofline=roof,
@@ -478,7 +494,8 @@ def run_leg(name: str, world: int, rank: int, local_rank: int, dist, steps: int,
                      (f" ({kern.p2p_note})" if getattr(kern, "p2p_note", None) else "")),
                phase=f"burn-in (sweeps {warmup + 1}..{warmup + steps})" if phase == "burnin" else
                      f"stored (burn-in 0, sweeps {warmup + 1}..{warmup + steps})",
-               clock_settle_ms=round(settle_s * 1e3, 1), gpu_clock_ghz=clk)
+               clock_settle_ms=round(settle_s * 1e3, 1), gpu_clock_ghz=clk, gpu_clock_source=clk_src,
+               gpu_clock_probe_ghz=clk_probe)
     if host_us:
         res["host_us"] = dict(host_us, clv_run_total=round(sum(host_us.values()), 3), timed_region=round(dt * 1e6, 3))
     if sharded:
@@ -507,7 +524,7 @@ def run_leg(name: str, world: int, rank: int, local_rank: int, dist, steps: int,
         sync()
         settle_clocks(settle_ms, local_rank)
         dt_st, kt_st = timed(steps, persistent)
-        clk_st = run_clock()
+        clk_st, clk_st_src, _ = run_clock()
         first = burnin + 101
         n_st = steps if persistent else min(steps, timing_steps)
         roof_st = launch_roofline(first, n_st, kt_st, "the timed stored launch" if persistent else
@@ -526,7 +543,7 @@ def run_leg(name: str, world: int, rank: int, local_rank: int, dist, steps: int,
                              hbm_frac_kernel=round(bk * v_st / 1e9 / (world * HBM_PEAK_GBS), 5),
                              bytes_note="bytes_per_unit / hbm_frac: SURVEY §8d (summary sinks +0 per stored sweep); "
                                         "*_kernel: the kernel's own bytes incl. the running sums' read-modify-write",
-                             roofline=roof_st, gpu_clock_ghz=clk_st)
+                             roofline=roof_st, gpu_clock_ghz=clk_st, gpu_clock_source=clk_st_src)
         if WORKLOADS[name][1].startswith("synthetic:"):
             t_b, t_s = dt / steps, dt_st / steps
             res["whole_run"] = dict(value=chains * n_total * (burnin + mcmc_workload) / (burnin * t_b + mcmc_workload * t_s),
@@ -643,6 +660,10 @@ def main():
         extra[leg] = run_leg(leg, world, rank, local_rank, dist, a.scaling_steps, 200, graph_chunk=a.graph_chunk,
                              exchange=exch, settle_ms=a.clock_settle_ms, stored_phase=a.stored_phase,
                              timing_steps=a.timing_steps)
+        if leg == "c4_shard8":
+            extra[leg]["note"] = ("NOT a BASELINE configuration: rank 0's shard of c4 at 8 ranks (distributed.plan(1M, 8): "
+                                  "126,976 customers, K=5, 1 chain) run at world size 1 — the per-GPU work of c4's "
+                                  "strong-scaling point without the exchange (DESIGN.md §6)")
         if world > 1 and leg == "c2":
             extra[leg]["note"] = ("NOT a BASELINE configuration: c2's 23,570 CDNOW customers tiled once per rank "
                                   "(a rehearsal of the CDNOW-size exchange at N GPUs)")
@@ -693,9 +714,13 @@ def main():
                         timed_region=prim["_timed_region"]),
             clock_settle_ms=prim["clock_settle_ms"],
             gpu_clock_ghz=prim.get("gpu_clock_ghz"),
-            gpu_clock_note="average shader clock of the timed clv_run (s_memtime / s_memrealtime between chain 0's "
-                           "level-2 publishes, clv_clock_ghz; persistent-kernel runs only, null for launch-per-sweep "
-                           "legs): boxes of one pool run the same cycles at clocks ~13% apart (DESIGN.md §8 round 5)",
+            gpu_clock_source=prim.get("gpu_clock_source"),
+            gpu_clock_probe_ghz=prim.get("gpu_clock_probe_ghz"),
+            gpu_clock_note="shader clock of the timed launches: the persistent kernel's own record (s_memtime / "
+                           "s_memrealtime between chain 0's level-2 publishes, clv_clock_ghz), else — launch-per-sweep "
+                           "legs — a 50 us probe kernel right behind them (clv_clock_probe; gpu_clock_probe_ghz on "
+                           "every line cross-checks the two): boxes of one pool run the same cycles at clocks ~13% "
+                           "apart (DESIGN.md §8 round 5)",
             roofline=prim["roofline"], cpu_baseline=cpu,
             host_us=prim.get("host_us"),
             cold=prim.get("cold"),

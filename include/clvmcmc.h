@@ -162,6 +162,12 @@ int64_t clv_sweeps_done(const clv_sampler* s);
  * MI355X boxes of one pool were measured to run the same cycles at clocks ~13% apart (DESIGN.md §8
  * round 5).  Synchronizes the sampler's stream. */
 int clv_clock_ghz(clv_sampler* s, double* ghz);
+/* Shader clock (GHz) read by a probe kernel enqueued on the sampler's stream behind whatever it runs
+ * (csrc/probe.hip): one 64-lane workgroup per CU busy for `us` microseconds (1..1e5) of s_memrealtime,
+ * s_memtime against s_memrealtime on each CU.  For legs whose kernel keeps no record of its own (the
+ * launch-per-sweep kernel): called right after the timed launches, it reads the clock they ran at
+ * (the governor moves on a millisecond scale).  Measurement only.  Synchronizes the stream. */
+int clv_clock_probe(clv_sampler* s, double us, double* ghz);
 /* How clv_run launches: out[6] = (persistent 0/1, persistent-kernel workgroups per CU, CUs,
  * workgroups per sweep, reserved (0), reserved (0)).
  * Persistent = one launch for all of a clv_run's sweeps with every customer block resident, chosen
@@ -201,6 +207,11 @@ int clv_p2p_connect(clv_sampler* s, const void* handles, const uint64_t* ptrs);
 /* Drop the peer connection (closes opened IPC mappings, forgets the peers' mail pointers): a sharded
  * clv_run then fails with CLV_ESTATE until clv_p2p_connect is called again.  Idempotent. */
 int clv_p2p_disconnect(clv_sampler* s);
+/* Which peer exchange clv_run takes on this shard: on = 1 the persistent kernel (only where its grid
+ * fits: clv_p2p_info out[4] as created), 0 the fused exchange (one sweep launch per sweep).  Both
+ * write the same mail with the same protocol and give the same bits; ShardedSampler falls back from
+ * the first to the second (then to RCCL) when the verification against RCCL fails. */
+int clv_p2p_set_persistent(clv_sampler* s, int32_t on);
 /* Bound of every wait in the persistent / fused-exchange kernels, in ms (default 2000 at world size
  * 1, 10000 with peers; the CLV_WAIT_TIMEOUT_MS environment variable sets the default at create).
  * A short bound makes a failed peer-exchange check cheap (distributed.ShardedSampler's verification

@@ -96,11 +96,13 @@ def lib() -> ctypes.CDLL:
         "clv_synchronize": (c_int32, [sp]),
         "clv_sweeps_done": (c_int64, [sp]),
         "clv_clock_ghz": (c_int32, [sp, POINTER(c_double)]),
+        "clv_clock_probe": (c_int32, [sp, c_double, POINTER(c_double)]),
         "clv_launch_info": (c_int32, [sp, POINTER(c_int64)]),
         "clv_p2p_info": (c_int32, [sp, POINTER(c_int64)]),
         "clv_p2p_export": (c_int32, [sp, c_void_p]),
         "clv_p2p_connect": (c_int32, [sp, c_void_p, POINTER(c_uint64)]),
         "clv_p2p_disconnect": (c_int32, [sp]),
+        "clv_p2p_set_persistent": (c_int32, [sp, c_int32]),
         "clv_set_wait_timeout": (c_int32, [sp, c_double]),
         "clv_set_stream": (c_int32, [sp, c_uint64]),
         "clv_note_sweeps": (c_int32, [sp, c_int64]),

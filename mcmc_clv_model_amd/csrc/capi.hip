@@ -328,26 +328,34 @@ bool clv::persist_grid_fits(int64_t grid_wgs, int blocks_per_cu, int n_cu) {
 }
 
 // Whether the persistent kernel is worth running a resident grid of grid_wgs workgroups (world size
-// 1 and the peer exchange): it holds every customer's state in registers and pays no launch per
-// sweep, but all its customer waves stay resident, so once most CUs hold two workgroups the
-// doubled SIMDs (two waves each, issue-bound) set every sweep's period, where the launch-per-sweep
-// kernel runs 4 waves per SIMD and load-balances.  Measured crossover (tools/persist_crossover.py,
-// profiles/r04_persist_crossover*.jsonl; us per sweep persistent / launch-per-sweep, workgroups
-// per CU):
-//   bivariate, 4 chains  K=2: 1.25 10.9 / 17.6, 1.61 12.6 / 18.7, 1.73 16.8 / 18.8, 1.86 19.6 / 19.5
-//                        K=5: 1.25 12.0 / 19.4, 1.61 13.9 / 20.4
-//   bivariate, 1-2 chains K=2: 0.92 8.0 / 15.7, 1.38 11.8 / 18.4, 1.68 22.8 / 19.5, 2 chains 1.84
-//                        23.6 / 19.2; K=5: 0.92 12.5 / 17.3, 1.38 21.0 / 20.8, 1.68 31.9 / 21.8,
-//                        1.91 43.8 / 22.4 (c4 at 8 ranks); K=9: 0.92 18.4 / 22.3, 1.38 29.9 / 29.8
-//   trivariate, 4 chains K=3: 1.25 12.5 / 20.3, 1.61 12.8 / 21.5; 1 chain K=3: 1.38 22.7 / 21.8,
-//                        1.68 26.7 / 23.1; K=9 (its persistent instance spills): 0.92 30.9 / 20.9
-// So: up to 1.75 workgroups per CU with 4+ chains, 1.45 (bivariate) / 1.25 (trivariate) with fewer,
-// never for the spilling trivariate instances (K >= 6).
+// 1 and the peer exchange).  Round 4 measured it losing to the launch-per-sweep kernel once most CUs
+// held two of its workgroups (c4's 8-rank shard, 1 chain x 497 workgroups: 43.8 vs 22.4 us per sweep)
+// and capped it by density.  The cause was not the doubled SIMDs: the level-2 workgroup emptied its
+// chain's hand-off slots lane-per-block (one double of a different line per lane and instruction), and
+// at ~500 blocks those ~7k partial-line write-throughs queued ahead of its draw (the draw measured 9.2
+// us of a 20 us sweep, profiles/r06_c4shard8_stamps_*.txt).  With coalesced resets (round 6) the
+// persistent kernel wins at every measured point (tools/persist_crossover.py,
+// profiles/r06_persist_crossover*.jsonl; us per sweep persistent / launch-per-sweep, workgroups per CU):
+//   bivariate, 4 chains  K=2: 1.25 10.1 / 17.1, 1.61 9.8 / 18.2, 1.73 9.9 / 18.3, 1.86 10.3 / 19.0
+//                        K=5: 1.25 10.4 / 18.5, 1.61 10.1 / 19.5
+//   bivariate, 1-2 chains K=2: 0.92 7.2 / 15.2, 1.38 10.1 / 17.6, 1.68 10.3 / 18.3, 2 chains 1.84
+//                        10.6 / 19.0; K=5: 0.92 9.2 / 16.6, 1.38 12.6 / 18.7, 1.68 13.8 / 19.6,
+//                        1.91 14.1 / 20.3 (c4 at 8 ranks); K=9: 0.92 12.8 / 18.4, 1.38 16.9 / 22.5
+//   trivariate, 4 chains K=3: 1.25 10.8 / 19.7, 1.61 11.5 / 20.7; 1 chain K=3: 1.38 14.6 / 19.6,
+//                        1.68 15.6 / 20.6; K=9 (its persistent instance spills): 0.92 20.1 / 20.8
+// So: wherever the grid fits (persist_grid_fits).  Kept as a function: the CPU test pins the choice.
+// Instances whose private segment (spills) exceeds this many bytes per lane are never run
+// persistently: the trivariate K = 9 peer instance (768 B per lane) at world 2 on one card left 39 of
+// a chain's 40 customer workgroups undispatched until its 10 s wait bound (round 6) — the runtime
+// provisions scratch for a limited number of waves, and a persistent grid must be resident whole.
+// Every instance a BASELINE configuration selects is at or below it: world size 1 0 B (bivariate K <=
+// 8, trivariate K <= 4), peer c2-tiled <2,2> 0 B, c4 at 8 ranks <2,5> 56 B, <3,3> 48 B (the tests'
+// world-3 trivariate run).  (llvm-readelf --notes: .private_segment_fixed_size.)
+constexpr size_t PERSIST_SCRATCH_MAX = 64;
+
 bool clv::persist_worth(int D, int K, int n_chains, int64_t grid_wgs, int n_cu) {
-  if (n_cu <= 0 || (D == 3 && K >= 6)) return false;
-  const double per_cu = (double)grid_wgs / n_cu;
-  const double cap = n_chains >= 4 ? 1.75 : (D == 2 ? 1.45 : 1.25);
-  return per_cu <= cap;
+  (void)D, (void)K, (void)n_chains;
+  return n_cu > 0 && grid_wgs > 0;
 }
 
 namespace {
@@ -362,6 +370,13 @@ namespace {
 // chain's level-2 workgroup (asleep most of the time) shares a CU with one of its own customer
 // workgroups, and the pairs are spread evenly over the chains.  Pure placement: every workgroup
 // still runs one logical (chain, block), so results do not depend on it.
+// Chains of at least CLV_L2_ALONE_MIN_NB blocks (the level-2 workgroup's lanes then poll two blocks
+// each) place their level-2 workgroup on a CU of its own: c4's 8-rank shard (496 blocks, 1 chain)
+// 13.54 -> 12.88 us per sweep; c2 (93 blocks per chain) 9.86 -> 9.80, within the noise, so it keeps
+// the pairing (profiles/r06_ab_l2alone.txt).
+#ifndef CLV_L2_ALONE_MIN_NB
+#define CLV_L2_ALONE_MIN_NB 256
+#endif
 std::vector<int32_t> persist_wg_map(int C, int nb, int n_cu) {
   const int per = nb + 1;  // workgroups per chain (block nb = the level-2 workgroup)
   const int T = C * per;
@@ -375,13 +390,15 @@ std::vector<int32_t> persist_wg_map(int C, int nb, int n_cu) {
     for (int b = nb - 1; b >= 0; --b) todo[c].push_back(b);
   std::vector<int32_t> first, second, single;
   int p = 0;
-  for (int c = 0; c < C && p < P; ++c, ++p) {  // level-2 workgroup + one own customer workgroup
+  const bool l2_alone = nb >= CLV_L2_ALONE_MIN_NB;
+  for (int c = 0; !l2_alone && c < C && p < P; ++c, ++p) {  // level-2 workgroup + one own customer workgroup
     first.push_back((c << 16) | nb);
     if (todo[c].empty()) return map;
     second.push_back((c << 16) | todo[c].back());
     todo[c].pop_back();
   }
-  const bool l2_paired = (int)first.size() == C;
+  const int n_l2_paired = (int)first.size();
+  const bool l2_paired = n_l2_paired == C;
   for (int c = 0; p < P; c = (c + 1) % C) {  // same-chain customer pairs, round robin over chains
     bool any = false;
     for (int k = 0; k < C && !any; ++k) any = todo[(c + k) % C].size() >= 2;
@@ -394,7 +411,7 @@ std::vector<int32_t> persist_wg_map(int C, int nb, int n_cu) {
     ++p;
   }
   for (int c = 0; c < C; ++c) {
-    if (!l2_paired && c >= (int)first.size()) single.push_back((c << 16) | nb);
+    if (!l2_paired && c >= n_l2_paired) single.push_back((c << 16) | nb);
     while (!todo[c].empty()) {
       single.push_back((c << 16) | todo[c].back());
       todo[c].pop_back();
@@ -529,13 +546,16 @@ int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* pri
   if (!s->replay && cfg->world_size == 1 && nb_local > 0 && bpu == 1 && nb_local <= 2 * BLOCK) {
     const char* env = std::getenv("CLV_PERSISTENT");
     hipDeviceProp_t prop{};
+    size_t scratch = SIZE_MAX;  // (a failed query: never persistent)
     if (persist_occupancy(g.D, g.K, false, &s->persist_bpc) == hipSuccess &&
+        persist_scratch_bytes(g.D, g.K, false, &scratch) == hipSuccess &&
         hipGetDeviceProperties(&prop, s->device) == hipSuccess)
       s->n_cu = prop.multiProcessorCount;
-    // CLV_PERSISTENT: "0" never, "1" whenever the grid fits (tests, A/B), unset: where it pays
+    // CLV_PERSISTENT: "0" never, "1" whenever the grid fits (tests, A/B), unset: where it pays;
+    // an instance that spills more than PERSIST_SCRATCH_MAX bytes per lane only when forced (tests)
     const int64_t grid = (int64_t)(nb_local + 1) * C;
     const bool force = env && std::string(env) == "1";
-    if ((!env || std::string(env) != "0") && persist_grid_fits(grid, s->persist_bpc, s->n_cu) &&
+    if ((!env || std::string(env) != "0") && (force || scratch <= PERSIST_SCRATCH_MAX) && persist_grid_fits(grid, s->persist_bpc, s->n_cu) &&
         (force || persist_worth(g.D, g.K, (int)C, grid, s->n_cu)))
       s->persistent = true;
   }
@@ -545,15 +565,17 @@ int clv_create(const clv_config* cfg, const clv_data* data, const clv_prior* pri
   if (!s->replay && cfg->world_size > 1 && cfg->world_size <= MAX_WORLD && nb_local > 0 && nb_local <= 2 * BLOCK && g.n_units_global <= 2 * BLOCK &&
       bpu <= 64 && (int64_t)g.stride * ((nb_local + bpu - 1) / bpu) <= UMAIL) {
     hipDeviceProp_t prop{};
+    size_t scratch = SIZE_MAX;  // (a failed query: never persistent)
     if (persist_occupancy(g.D, g.K, true, &s->persist_bpc) == hipSuccess &&
+        persist_scratch_bytes(g.D, g.K, true, &scratch) == hipSuccess &&
         hipGetDeviceProperties(&prop, s->device) == hipSuccess)
       s->n_cu = prop.multiProcessorCount;
     const char* env = std::getenv("CLV_PERSISTENT");  // "0": the fused exchange below instead
     const int64_t grid = (int64_t)(nb_local + 1) * C;
     const bool force = env && std::string(env) == "1";
-    if ((!env || std::string(env) != "0") && persist_grid_fits(grid, s->persist_bpc, s->n_cu) &&
+    if ((!env || std::string(env) != "0") && (force || scratch <= PERSIST_SCRATCH_MAX) && persist_grid_fits(grid, s->persist_bpc, s->n_cu) &&
         (force || persist_worth(g.D, g.K, (int)C, grid, s->n_cu)))
-      s->p2p_capable = true;
+      s->p2p_capable = s->p2p_persist_fits = true;
   }
   // Any other shard: the sweep kernel's fused level-2 tail exchanges through the same mail (one
   // launch per sweep, no host collective; n_units_global <= 2 CLV_BLOCK as its readers assume)
@@ -919,6 +941,17 @@ int clv_p2p_connect(clv_sampler* s, const void* handles, const uint64_t* ptrs) {
   CLV_HIP(hipMemcpy(s->d_peers, peers.data(), sizeof(double*) * W, hipMemcpyHostToDevice));
   CLV_HIP(hipStreamSynchronize(s->stream));  // the mail's sentinel fill has landed
   s->p2p_ready = true;
+  return CLV_OK;
+}
+
+int clv_p2p_set_persistent(clv_sampler* s, int32_t on) {
+  if (!s) return fail(CLV_EINVAL, "null sampler");
+  if (on && !s->p2p_persist_fits) return fail(CLV_ESTATE, "the persistent peer exchange does not fit this shard's grid");
+  if (!on && !s->fx_capable) return fail(CLV_ESTATE, "no fused peer exchange for this sampler");
+  CLV_HIP(hipSetDevice(s->device));
+  CLV_HIP(hipStreamSynchronize(s->stream));
+  s->p2p_capable = on != 0;
+  s->last_persist_n = 0;  // (a rollback undoes a call of the path that ran it)
   return CLV_OK;
 }
 

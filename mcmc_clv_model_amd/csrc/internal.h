@@ -132,6 +132,7 @@ struct clv_sampler {
   int persist_bpc = 0, n_cu = 0;    // persist_kernel occupancy (workgroups per CU), CUs
   // world size > 1: persistent kernel with the peer (xGMI) exchange
   bool p2p_capable = false;         // the grid fits at once and the unit partials fit UMAIL
+  bool p2p_persist_fits = false;    // (p2p_capable as chosen at create; clv_p2p_set_persistent may clear p2p_capable)
   bool fx_capable = false;          // fused peer exchange (launch-per-sweep, any shard size)
   bool p2p_ready = false;           // clv_p2p_connect done: clv_run runs persist_kernel
   double* d_mail = nullptr;         // [2][world][chain][units_per_rank][stride]

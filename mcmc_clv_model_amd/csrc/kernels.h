@@ -162,6 +162,7 @@ hipError_t launch_group(const GroupArgs& a, hipStream_t st);
 hipError_t launch_persist(const SweepArgs& a, int64_t s_first, int64_t n_sweeps, hipStream_t st,
                           hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 hipError_t persist_occupancy(int D, int K, bool p2p, int* blocks_per_cu);
+hipError_t persist_scratch_bytes(int D, int K, bool p2p, size_t* bytes);  // spilled instances: > 0
 // The deferred level-2 draw alone (a.pend_in, no sweeps): one level-2 workgroup per chain.
 hipError_t launch_persist_flush(const SweepArgs& a, int64_t s_first, hipStream_t st);
 hipError_t launch_hyper(const HyperArgs& a, bool replay, hipStream_t st);

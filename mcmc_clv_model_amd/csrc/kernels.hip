@@ -2372,19 +2372,24 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
     // 4. reset: the partial slots (their writers write again only after step 6) and the
     //    (beta, Sigma) set every reader of s has read (its next write is for s+2; at sweep s_first
     //    of a launch that drew a deferred draw first, its readers took it from this slot too)
-#pragma unroll
-    for (int j = 0; j < NS; ++j) {
-      if (hb0) st_wt(pb0 + j, slot_empty());
-      if (hb1) st_wt(pb1 + j, slot_empty());
+    //    Coalesced: consecutive lanes empty consecutive doubles of the chain's [block][stat] slots
+    //    (round 6).  Lane-per-block resets (lane b: its block's NS doubles) wrote one double of a
+    //    different line per lane and instruction — c4's 8-rank shard (496 blocks x 14 statistics)
+    //    queued ~7k partial-line write-throughs ahead of the draw on this wave: 8.2 us of a 20 us
+    //    sweep (profiles/r06_c4shard8_stamps_*.txt).
+    {
+      const int nrec = g.nb_local * NS;
+      for (int e = tid; e < nrec; e += NT) st_wt(parts + e, slot_empty());
     }
     if ((it > 0 || pin) && tid < HS) st_wt(a.hyp2 + ((int64_t)(s & 1) * g.n_chains + c) * HS + tid, slot_empty());
     if constexpr (P2P) {  // this rank's mail slots of sweep s: empty again before any rank can
                           // write sweep s + 2 there (only after this rank's units of s + 1, which
-                          // leave after the vmcnt(0) below)
-#pragma unroll
-      for (int j = 0; j < NS; ++j) {
-        if (m0) st_sys((double*)p0 + j, slot_empty());
-        if (m1) st_sys((double*)p1 + j, slot_empty());
+                          // leave after the vmcnt(0) below); every other rank's [unit][stat] run of
+                          // this (parity, chain), coalesced like the block slots
+      const int nrun = g.units_per_rank * NS;
+      for (int e = tid; e < g.world_size * nrun; e += NT) {
+        const int q = e / nrun;
+        if (q != a.rank) st_sys((double*)mb + (int64_t)q * per_rank + (e - q * nrun), slot_empty());
       }
     }
     }  // (!from_pend)
@@ -2908,6 +2913,27 @@ hipError_t launch_persist(const SweepArgs& a, int64_t s_first, int64_t n_sweeps,
 hipError_t persist_occupancy(int D, int K, bool p2p, int* blocks_per_cu) {
 #define CLV_CASE(DD, KK, PP) \
   if (D == DD && K == KK && p2p == PP) return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, persist_kernel<DD, KK, PP>, BLOCK, 0);
+  CLV_FOR_K(CLV_CASE, 2, false)
+  CLV_FOR_K(CLV_CASE, 3, false)
+  CLV_FOR_K(CLV_CASE, 2, true)
+  CLV_FOR_K(CLV_CASE, 3, true)
+#undef CLV_CASE
+  return hipErrorInvalidValue;
+}
+
+// Private-segment (scratch) bytes per lane of a persistent instance: > 0 where the compiler spilled
+// (trivariate K >= 6 at world size 1, large trivariate K in the peer instances).  Such a grid is not
+// run persistently: the runtime may cap the waves in flight by the scratch it provisions, and a
+// resident grid that is not all resident deadlocks its hand-offs until the wait bound (seen: the
+// trivariate K = 9 peer instance at world 2 on one card, round 6).
+hipError_t persist_scratch_bytes(int D, int K, bool p2p, size_t* bytes) {
+  hipFuncAttributes fa{};
+#define CLV_CASE(DD, KK, PP)                                                                     \
+  if (D == DD && K == KK && p2p == PP) {                                                         \
+    const hipError_t e = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&persist_kernel<DD, KK, PP>)); \
+    *bytes = fa.localSizeBytes;                                                                  \
+    return e;                                                                                    \
+  }
   CLV_FOR_K(CLV_CASE, 2, false)
   CLV_FOR_K(CLV_CASE, 3, false)
   CLV_FOR_K(CLV_CASE, 2, true)

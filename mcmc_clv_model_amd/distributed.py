@@ -235,51 +235,70 @@ class ShardedSampler:
             return
         handles = [None] * self.world
         dist.all_gather_object(handles, self.s.p2p_export(), group=self.group)
-        err = None
-        try:
-            self.s.p2p_connect(handles=handles)
-        except Exception as e:  # noqa: BLE001 - reported below, on every rank
-            err = e
-        if not self._all_ok(err is None):
-            if required:
-                raise _lib.ClvError(f"p2p exchange: connect failed ({err})")
-            self.p2p_note = f"connect failed ({err})"
-            return
-        dist.barrier(group=self.group)
-        if verify_sweeps > 0:
-            n0 = self.s.sweeps_done
-            snap = self.s.get_state()
-            self._eager(verify_sweeps)
-            self.synchronize()
-            ref = self.s.get_state()
-            self.s.set_state(*snap, n0)
-            dist.barrier(group=self.group)
+        # the persistent peer exchange first where every rank's grid fits, then the fused one (one
+        # sweep launch per sweep, same mail and bits), then RCCL: each path is kept only once it has
+        # reproduced the RCCL path's state bitwise on every rank
+        paths = ([True] if self._all_ok(self.s.p2p_info()["persistent"]) else []) + [False]
+        notes = []
+        for persistent in paths:
             err = None
-            # the ranks leave the barrier together, so the check's launches start within
-            # milliseconds of each other: a short wait bound makes a failed check cost well under
-            # a second instead of the run's 10 s bound (which absorbs host-side skew later on)
-            self.s.set_wait_timeout(VERIFY_WAIT_MS)
             try:
-                self.s.run(verify_sweeps)
-                got = self.s.get_state()
-                same = all(np.array_equal(a.view(np.uint64), b.view(np.uint64)) for a, b in zip(ref, got))
-            except Exception as e:  # noqa: BLE001
-                same, err = False, e
-            finally:
-                try:  # never mask the verification's outcome with an exception from the restore
-                    self.s.set_wait_timeout(run_wait_ms())
-                except Exception as e:  # noqa: BLE001
-                    err = err or e
-            if not self._all_ok(same):
-                self.s.set_state(*snap, n0)  # the RCCL path carries on from the same state
-                if required:
-                    raise _lib.ClvError(f"p2p exchange: verification against RCCL failed ({err or 'state differs'})")
-                self.p2p_note = f"verification against RCCL failed ({err or 'state differs'})"
-                return
-            self.s.set_state(*snap, n0)
+                self.s.p2p_set_persistent(persistent)
+                self.s.p2p_connect(handles=handles)
+            except Exception as e:  # noqa: BLE001 - reported below, on every rank
+                err = e
+            kind = "persistent" if persistent else "fused"
+            if not self._all_ok(err is None):
+                notes.append(f"{kind}: connect failed ({err})")
+                continue
             dist.barrier(group=self.group)
-        self.exchange = "p2p"
-        self.p2p_note = f"verified bitwise against RCCL over {verify_sweeps} sweeps" if verify_sweeps > 0 else None
+            ok, err = self._verify_p2p(verify_sweeps) if verify_sweeps > 0 else (True, None)
+            if ok:
+                self.exchange = "p2p"
+                self.p2p_note = "; ".join(notes + [f"{kind} exchange" + (
+                    f" verified bitwise against RCCL over {verify_sweeps} sweeps" if verify_sweeps > 0 else "")])
+                return
+            notes.append(f"{kind}: verification against RCCL failed ({err or 'state differs'})")
+        try:
+            self.s.p2p_disconnect()
+        except Exception:  # noqa: BLE001
+            pass
+        if required:
+            raise _lib.ClvError("p2p exchange: " + "; ".join(notes))
+        self.p2p_note = "; ".join(notes)
+
+    def _verify_p2p(self, verify_sweeps: int):
+        """Run ``verify_sweeps`` sweeps through the RCCL path and, from the same state, through the
+        connected peer path; (True, None) iff every rank's state is bitwise identical.  The state is
+        restored either way, and the ranks leave in step."""
+        import torch.distributed as dist
+        n0 = self.s.sweeps_done
+        snap = self.s.get_state()
+        self._eager(verify_sweeps)
+        self.synchronize()
+        ref = self.s.get_state()
+        self.s.set_state(*snap, n0)
+        dist.barrier(group=self.group)
+        err = None
+        # the ranks leave the barrier together, so the check's launches start within
+        # milliseconds of each other: a short wait bound makes a failed check cost well under
+        # a second instead of the run's 10 s bound (which absorbs host-side skew later on)
+        self.s.set_wait_timeout(VERIFY_WAIT_MS)
+        try:
+            self.s.run(verify_sweeps)
+            got = self.s.get_state()
+            same = all(np.array_equal(a.view(np.uint64), b.view(np.uint64)) for a, b in zip(ref, got))
+        except Exception as e:  # noqa: BLE001
+            same, err = False, e
+        finally:
+            try:  # never mask the verification's outcome with an exception from the restore
+                self.s.set_wait_timeout(run_wait_ms())
+            except Exception as e:  # noqa: BLE001
+                err = err or e
+        ok = self._all_ok(same)
+        self.s.set_state(*snap, n0)  # (the chosen path, or the next, carries on from the same state)
+        dist.barrier(group=self.group)
+        return ok, err
 
     def _exchange_and_hyper(self) -> None:
         with self.torch.cuda.stream(self.cur):
@@ -347,9 +366,15 @@ class ShardedSampler:
         return info
 
     def clock_ghz(self) -> float:
-        """This rank's average shader clock over its last clv_run (p2p / fused exchange); 0.0 on the
-        RCCL path, which runs clv_sweep / clv_hyper and keeps no record."""
+        """This rank's average shader clock over its last clv_run as the persistent kernel records it
+        (p2p exchange with a resident grid); 0.0 where nothing was recorded: the fused exchange's
+        launch-per-sweep kernel and the RCCL path (clv_sweep / clv_hyper) keep no record — see
+        clock_probe."""
         return self.s.clock_ghz() if self.exchange == "p2p" else 0.0
+
+    def clock_probe(self, us: float = 50.0) -> float:
+        """This rank's shader clock read by a probe kernel behind its launches (clv_clock_probe)."""
+        return self.s.clock_probe(us)
 
     def set_timing(self, enable: bool) -> None:
         self.timing = bool(enable)

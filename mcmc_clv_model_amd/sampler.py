@@ -250,10 +250,19 @@ class HipSampler:
         return {k: round(h[i + 1] - h[i], 3) for i, k in enumerate(names)}
 
     def clock_ghz(self) -> float:
-        """clv_clock_ghz: the average shader clock (GHz) over the last run() (0.0 when not recorded:
-        fewer than 3 sweeps, or the RCCL-sharded path)."""
+        """clv_clock_ghz: the average shader clock (GHz) over the last run(), recorded by the
+        persistent kernel; 0.0 when nothing was recorded (a run of fewer than 2 sweeps, or one
+        without the persistent kernel: the launch-per-sweep kernel keeps no record — see
+        clock_probe)."""
         v = ctypes.c_double(0.0)
         check(self._L.clv_clock_ghz(self.h, ctypes.byref(v)))
+        return float(v.value)
+
+    def clock_probe(self, us: float = 50.0) -> float:
+        """clv_clock_probe: the shader clock (GHz) read by a `us`-microsecond probe kernel enqueued
+        on this sampler's stream behind the launches already there (csrc/probe.hip)."""
+        v = ctypes.c_double(0.0)
+        check(self._L.clv_clock_probe(self.h, float(us), ctypes.byref(v)))
         return float(v.value)
 
     def launch_info(self) -> dict:
@@ -288,6 +297,10 @@ class HipSampler:
         else:
             arr = (ctypes.c_uint64 * len(ptrs))(*[int(p) for p in ptrs])
             check(self._L.clv_p2p_connect(self.h, None, arr))
+
+    def p2p_set_persistent(self, on: bool) -> None:
+        """clv_p2p_set_persistent: the persistent peer exchange (where its grid fits) or the fused one."""
+        check(self._L.clv_p2p_set_persistent(self.h, 1 if on else 0))
 
     def p2p_disconnect(self) -> None:
         """clv_p2p_disconnect: forget the peers' mail (a sharded run() needs p2p_connect again)."""

@@ -217,6 +217,15 @@ with HipSampler(p, **kw) as s:          # unsharded reference, before any rank's
     ref = s.get_state()
     ref_sums = s.read_summary()[0]
 dist.init_process_group("gloo")
+if os.environ.get("CLV_TEST_STALL_PERSISTENT_RANK") == str(rank):
+    # test hook: this rank's persistent launches never run (its peer's wait times out), fused ones do
+    from mcmc_clv_model_amd import _lib, sampler as S
+    run0 = S.HipSampler.run
+    def run(self, n):
+        if self.p2p_info()["persistent"]:
+            raise _lib.ClvError("test hook: persistent launch withheld")
+        return run0(self, n)
+    S.HipSampler.run = run
 ss = ShardedSampler(p, rank=rank, world=world, device=0, exchange="p2p", verify_sweeps=4, **kw)
 ss.step(9)
 ss.step(8)
@@ -232,11 +241,13 @@ dist.destroy_process_group()
 """
 
 
-@pytest.mark.parametrize("D,persistent", [(2, "1"), (3, "1"), (2, "0")])
-def test_p2p_two_processes_ipc(D, persistent):
+@pytest.mark.parametrize("D,persistent,stall", [(2, "1", None), (3, "1", None), (2, "0", None), (2, "1", 1)])
+def test_p2p_two_processes_ipc(D, persistent, stall):
     """Two processes (one rank each) on the one GPU: hipIpcMemHandle exchange, verification
     against the all-gather path, then 17 sweeps in two steps — bitwise equal to the unsharded run
-    (persistent = "0": through the fused exchange)."""
+    (persistent = "0": through the fused exchange).  stall = 1: rank 1 withholds its persistent
+    launches, so the persistent exchange fails its verification on both ranks and ShardedSampler
+    falls back to the fused exchange (round 6), verified the same way, before RCCL."""
     with socket.socket() as so:
         so.bind(("127.0.0.1", 0))
         port = so.getsockname()[1]
@@ -244,6 +255,8 @@ def test_p2p_two_processes_ipc(D, persistent):
     for r in range(2):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port), CLV_ROOT=ROOT, CLV_D=str(D), CLV_PERSISTENT=persistent)
+        if stall is not None:
+            env["CLV_TEST_STALL_PERSISTENT_RANK"] = str(stall)
         procs.append(subprocess.Popen([sys.executable, "-c", WORKER], env=env, cwd=ROOT, stdout=subprocess.PIPE,
                                       stderr=subprocess.PIPE, text=True))
     outs = []
@@ -260,6 +273,12 @@ def test_p2p_two_processes_ipc(D, persistent):
         import json
         res = json.loads(out.strip().splitlines()[-1])
         assert res["ok"], res
+        if stall is not None:
+            assert "persistent: verification against RCCL failed" in res["note"], res
+            assert res["note"].endswith("fused exchange verified bitwise against RCCL over 4 sweeps"), res
+        else:
+            kind = "persistent" if persistent == "1" else "fused"
+            assert res["note"] == f"{kind} exchange verified bitwise against RCCL over 4 sweeps", res
 
 
 @pytest.mark.parametrize("persistent", ["1", "0"])

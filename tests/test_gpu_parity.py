@@ -312,7 +312,8 @@ def test_clock_record_persistent_and_launch_per_sweep(L):
     """clv_clock_ghz: the shader clock over a run of the persistent kernel, from chain 0's level-2
     workgroup's (s_memtime, s_memrealtime) between publishes (per-CU intervals: s_memtime counts per
     XCD); 0 for a one-sweep run and for the launch-per-sweep kernel, which keeps no record.  MI355X's
-    engine clock is at most 2.4 GHz."""
+    engine clock is at most 2.4 GHz.  clv_clock_probe (a 50 us probe kernel behind the run) reads
+    it for either kernel and agrees with the persistent kernel's record."""
     from mcmc_clv_model_amd.sampler import HipSampler, build_problem
     from mcmc_clv_model_amd.data import synthetic_cbs
     cases = [(build_problem(cdnow("full"), ["first_sales_scaled"], 2), 4, True),
@@ -324,11 +325,14 @@ def test_clock_record_persistent_and_launch_per_sweep(L):
             assert s.clock_ghz() == 0.0
             s.run(200)
             ghz = s.clock_ghz()
-            print(f"persistent={persistent}: {ghz:.3f} GHz")
+            probe = s.clock_probe(50.0)  # verdict r5 #6: every leg's clock, the probe kernel behind the run
+            print(f"persistent={persistent}: record {ghz:.3f} GHz, probe {probe:.3f} GHz")
+            assert 0.5 < probe < 2.6
             if not persistent:
                 assert ghz == 0.0
                 continue
             assert 0.5 < ghz < 2.6
+            assert abs(probe / ghz - 1) < 0.1  # the two readings of one clock
             s.run(1500)  # longer than the record (the last 1024 sweeps)
             assert 0.5 < s.clock_ghz() < 2.6
 

@@ -94,12 +94,12 @@ def test_persistent_residency_margin():
 
 
 def test_persistent_choice_by_grid_density():
-    """Verdict r3 #8: which grids run the persistent kernel (world size 1, and the peer exchange at
-    world size > 1).  Measured (tools/persist_crossover.py): once most CUs hold two of its
-    workgroups it loses to the launch-per-sweep kernel — c4's 8-rank shard (1 chain, 496 blocks +
-    1 level-2 workgroup = 497 of 504 slots; persist_kernel<2,5,true>, 256 VGPRs) would run ~2x
-    slower than the fused exchange, so it takes the fused exchange; c2 / c3 (4 x 94 = 376), c2 tiled
-    per rank at 8 ranks (the same 376) and c1 keep it."""
+    """Verdict r3 #8 / r5 #4: which grids run the persistent kernel (world size 1, and the peer
+    exchange at world size > 1).  Round 4's density cap came from the level-2 workgroup's
+    lane-per-block slot resets (~7k partial-line write-throughs ahead of its draw at ~500 blocks);
+    with coalesced resets the persistent kernel wins at every measured density
+    (profiles/r06_persist_crossover*.jsonl: c4's 8-rank shard, 1 chain x 497 workgroups, 14.1 vs
+    20.3 us per sweep), so it runs wherever the grid fits — c4 at 8 ranks included."""
     from mcmc_clv_model_amd import _lib
     from mcmc_clv_model_amd.distributed import plan
     L = _lib.lib()
@@ -108,15 +108,10 @@ def test_persistent_choice_by_grid_density():
     assert pick(2, 1, 4, 4 * (10 + 1))                                      # c1 (2,357 customers)
     p8 = plan(1_000_000, 8)
     nb_rank = -(-(p8.shard(0)[1] - p8.shard(0)[0]) // 256)
-    assert nb_rank == 496 and L.clv_debug_persist_fits(nb_rank + 1, 2, 256)  # it would fit ...
-    assert not pick(2, 5, 1, nb_rank + 1)                                   # ... but is not chosen
-    assert not pick(2, 5, 1, 490) and pick(2, 5, 1, 236)                    # measured: 43.8 vs 22.4 / 12.5 vs 17.3 us
-    assert pick(2, 2, 4, 444) and not pick(2, 2, 4, 476)                    # 16.8 vs 18.8 / 19.6 vs 19.5 us
-    assert pick(2, 2, 1, 353) and not pick(2, 2, 1, 431)                    # 11.8 vs 18.4 / 22.8 vs 19.5 us
-    assert not pick(2, 2, 2, 472)                                           # 23.6 vs 19.2 us
-    assert not pick(3, 3, 1, 353) and pick(3, 3, 4, 412)                    # 22.7 vs 21.8 / 12.8 vs 21.5 us
-    assert not pick(3, 9, 1, 236)                                           # spilling instance: 30.9 vs 20.9 us
-    assert not pick(2, 2, 4, 505)                                           # does not fit at all
+    assert nb_rank == 496 and pick(2, 5, 1, nb_rank + 1)                    # c4 at 8 ranks: 14.1 vs 20.3 us
+    assert pick(2, 2, 4, 476) and pick(2, 2, 2, 472) and pick(3, 3, 1, 431)  # 10.3 / 19.0, 10.6 / 19.0, 15.6 / 20.6
+    assert pick(3, 9, 1, 236)                                               # spilling instance: 20.1 vs 20.8 us
+    assert not pick(2, 2, 4, 505) and not pick(2, 5, 1, 505)                # does not fit at all
 
 
 def test_no_cpu_fallback_without_gpu():
@@ -300,13 +295,14 @@ def test_philox_header_host_build_kat_and_hoisting(tmp_path):
 
 
 @pytest.mark.parametrize("C,nb,n_cu", [(4, 93, 256), (3, 93, 256), (4, 94, 256), (2, 200, 256), (8, 40, 256),
-                                       (1, 300, 256), (4, 40, 256), (4, 200, 256)])
+                                       (1, 300, 256), (4, 40, 256), (4, 200, 256), (1, 496, 256)])
 def test_persistent_placement_map(C, nb, n_cu):
     """clv_debug_wg_map (host code, capi.hip persist_wg_map): the placement of the persistent grid is
     a permutation of every (chain, block) incl. each chain's level-2 workgroup; when the grid has
     more workgroups than CUs (but at most two per CU), the workgroups dispatched onto the same CU
     (linear i and i + n_cu) belong to the same chain, and each level-2 workgroup shares its CU with
-    one of its own chain's customer workgroups; otherwise the identity."""
+    one of its own chain's customer workgroups (chains of >= 256 blocks: alone on a CU, round 6);
+    otherwise the identity."""
     from mcmc_clv_model_amd import _lib
     L = _lib.lib()
     T = C * (nb + 1)
@@ -322,7 +318,10 @@ def test_persistent_placement_map(C, nb, n_cu):
     for i in range(P):
         assert chain[i] == chain[i + n_cu], (i, chain[i], chain[i + n_cu])
     l2 = np.flatnonzero(block == nb)
-    assert all(i < P or i >= n_cu for i in l2)  # every level-2 workgroup sits on a shared CU
+    if nb >= 256:  # (CLV_L2_ALONE_MIN_NB) its lanes poll two blocks each: the level-2 workgroup alone on a CU
+        assert all(P <= i < n_cu for i in l2)
+    else:  # every level-2 workgroup sits on a shared CU, beside one of its chain's customer workgroups
+        assert all(i < P or i >= n_cu for i in l2)
     pairs = np.bincount(chain[:P], minlength=C)
     assert pairs.max() - pairs.min() <= 1  # shared CUs spread evenly over the chains
 
@@ -580,7 +579,10 @@ def test_bench_config_times_the_stored_phase(monkeypatch):
             return dict(sweep_ms=0.085 * n, sweep_launches=n, hyper_ms=0.0, hyper_launches=0)
 
         def clock_ghz(self):
-            return 2.25
+            return 0.0  # the launch-per-sweep kernel keeps no record ...
+
+        def clock_probe(self, us):
+            return 2.25  # ... so the line takes the probe kernel's reading
 
         def close(self):
             pass
@@ -612,7 +614,8 @@ def test_bench_config_times_the_stored_phase(monkeypatch):
     assert "c4stored" in r["stored"]["roofline"]["bound_evidence"]["source"]
     assert r["stored"]["roofline"]["traffic"] != roof["traffic"] and "running sums" in r["stored"]["roofline"]["traffic_note"]
     assert bench.profile_name("c5", "stored") == "c5stored" and bench.profile_name("c5", "burnin") == "c5"
-    assert r["gpu_clock_ghz"] == 2.25 and r["stored"]["gpu_clock_ghz"] == 2.25  # clv_clock_ghz of the timed runs
+    assert r["gpu_clock_ghz"] == 2.25 and r["stored"]["gpu_clock_ghz"] == 2.25  # verdict r5 #6: a clock on every leg
+    assert r["gpu_clock_source"].startswith("clv_clock_probe") and r["gpu_clock_probe_ghz"] == 2.25
     tb, ts = r["ms_per_step"], r["stored"]["ms_per_step"]
     n = 500
     want = n * 10000 / (5000 * tb + 5000 * ts) * 1e3
@@ -632,7 +635,8 @@ def test_bench_primary_is_a_baseline_configuration():
     for n in (2, 4, 8):
         assert bench.primary_workload(n) == "c5" and bench.BASELINE_INDEX["c5"] == 4
         assert bench.config_legs(n, "c5") == ["c4", "c2"]
-    assert bench.config_legs(1, "c2") == ["c3", "c4", "c5"]
+    assert bench.config_legs(1, "c2") == ["c3", "c4", "c5", "c4_shard8"]
+    assert bench.WORKLOADS["c4_shard8"][1].endswith(":shard0of8") and "c4_shard8" not in bench.BASELINE_INDEX
     assert bench.survey_bytes(2, 2, 0.1, "full") == pytest.approx(63.2) and \
         bench.survey_bytes(3, 3, 0.1, "full") == pytest.approx(96.0)
     assert bench.survey_bytes(2, 5, 1.0, "summary") == 84.0 and bench.survey_bytes(3, 9, 1.0, "summary") == 140.0
