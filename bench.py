@@ -707,7 +707,7 @@ def main():
                   f"CDNOW {data} CBS ({n_total // world:,} real customers, tests/golden/cdnow_{data}_cbs.npz)"
                   + ("" if world == 1 else f", tiled x{world} (one copy per rank)")),
             config=dict(workload=f"{name}: {'bivariate' if D == 2 else 'trivariate'} M2, covariates {covs}",
-                        baseline_config=BASELINE_INDEX[name],
+                        baseline_config=BASELINE_INDEX.get(name),
                         n_customers=n_total, chains=chains, n_mh_steps=20, burnin=burnin, mcmc=mcmc,
                         thin=thin, seed=42, draw_sink=sink, parallelism=f"customer-shard x{world}",
                         **({"phase": "stored (profiling: burn-in 0, every sweep stores)"} if a.phase == "stored" else {}),

@@ -14,6 +14,7 @@ for W in "$@"; do
   WL=${W%stored}; PH=burnin; [ "$WL" != "$W" ] && PH=stored
   case $WL in
     c2|c3|c1) TR="--steps 19000 --warmup 5"; PS=20000 ;;  # PMC: the whole 20,000-sweep workload, one dispatch
+    c4_shard8) TR="--steps 9000 --warmup 5"; PS=10000 ;;  # (persistent since round 6: its 10,000-sweep run)
     *)        TR="--steps 2000 --warmup 200 --timing-steps 500"; PS=100 ;;
   esac
   B="python3 $R/bench.py --workload $WL --phase $PH --no-cpu-baseline --scaling-configs= --no-c1-leg --no-stored-phase --no-whole-run"
