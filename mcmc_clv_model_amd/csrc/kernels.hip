@@ -972,13 +972,21 @@ __device__ __forceinline__ void hyper_sum_units(const HyperArgs& a, int c, const
 }
 
 // Part 3: the workgroup reduction of the lanes' sums, the algebra and the outputs.
-template <int D, int K, bool REPLAY, int NS, int NT>
+struct NoWork {
+  __device__ void operator()() const {}
+};
+
+// after_reduce: work for the other wavefronts once the sums are formed (the fused exchange empties
+// its mail slots there), run while wavefront 0 draws; no barrier follows it here.
+template <int D, int K, bool REPLAY, int NS, int NT, class After = NoWork>
 __device__ void hyper_finish(const HyperArgs& a, int c, int64_t s, int mode, double (&acc)[NS], double (*red)[NS],
-                             double* tot, double* var_iw, double* var_chi, double* var_noise, L2Scratch* l2) {
+                             double* tot, double* var_iw, double* var_chi, double* var_noise, L2Scratch* l2,
+                             After after_reduce = After{}) {
   const Geometry& g = a.g;
   const int tid = threadIdx.x;
   const int64_t hs = (D == 2) ? s + 1 : s;
   block_reduce<NS, NT>(acc, red, tot);  // its barriers also publish the variates written to LDS above
+  after_reduce();
 
   // algebra (element-parallel phases + one-lane core) and outputs
   if (tid == 0) CLV_STAMP(a.stamps, s, 6, false);
@@ -2043,12 +2051,18 @@ __device__ __forceinline__ void sweep_body(const SweepArgs& a) {
         if (timed_out) s_fx_abort = 1;
         __syncthreads();
         if (!s_fx_abort) {
-#pragma unroll
-          for (int j = 0; j < NS; ++j) {
-            if (h0) st_sys(p0 + j, slot_empty());
-            if (h1) st_sys(p1 + j, slot_empty());
-          }
-          hyper_finish<D, K, REPLAY, NS, NT>(a.h, c, s, 0, acc, red, tot, var_iw, var_chi, var_noise, &l2);
+          // the slots of sweep s empty again for sweep s + 2 (written only after the next kernel
+          // boundary): every rank's [unit][stat] run of this (parity, chain), coalesced, by
+          // wavefronts 1-3 while wavefront 0 draws — lane-per-unit resets wrote one double of a
+          // different line per lane and instruction ahead of the draw (c5 at 8 ranks: 306 units x
+          // 34 statistics; round 6, as the persistent kernel's slots)
+          const int nrun = g.units_per_rank * NS;
+          hyper_finish<D, K, REPLAY, NS, NT>(a.h, c, s, 0, acc, red, tot, var_iw, var_chi, var_noise, &l2, [&] {
+            for (int e = (int)threadIdx.x - 64; e >= 0 && e < g.world_size * nrun; e += NT - 64) {
+              const int q = e / nrun;
+              st_sys((double*)mb + (int64_t)q * mail_rank + (e - q * nrun), slot_empty());
+            }
+          });
         }
       }
       if (threadIdx.x == 0) CLV_STAMP(a.stamps, s, 3, false);
@@ -2376,18 +2390,21 @@ __device__ __forceinline__ void persist_level2(const SweepArgs& a, int64_t s_fir
     //    (round 6).  Lane-per-block resets (lane b: its block's NS doubles) wrote one double of a
     //    different line per lane and instruction — c4's 8-rank shard (496 blocks x 14 statistics)
     //    queued ~7k partial-line write-throughs ahead of the draw on this wave: 8.2 us of a 20 us
-    //    sweep (profiles/r06_c4shard8_stamps_*.txt).
-    {
+    //    sweep (profiles/r06_c4shard8_stamps_*.txt).  Issued by wavefronts 1-3 only, while wavefront 0
+    //    runs the draw (step 5): its instructions queue behind none of them (the vmcnt(0) before
+    //    the publish waits for them all).
+    const int rt = tid - 64;  // (< 0: wavefront 0)
+    if (rt >= 0) {
       const int nrec = g.nb_local * NS;
-      for (int e = tid; e < nrec; e += NT) st_wt(parts + e, slot_empty());
+      for (int e = rt; e < nrec; e += NT - 64) st_wt(parts + e, slot_empty());
+      if ((it > 0 || pin) && rt < HS) st_wt(a.hyp2 + ((int64_t)(s & 1) * g.n_chains + c) * HS + rt, slot_empty());
     }
-    if ((it > 0 || pin) && tid < HS) st_wt(a.hyp2 + ((int64_t)(s & 1) * g.n_chains + c) * HS + tid, slot_empty());
     if constexpr (P2P) {  // this rank's mail slots of sweep s: empty again before any rank can
                           // write sweep s + 2 there (only after this rank's units of s + 1, which
                           // leave after the vmcnt(0) below); every other rank's [unit][stat] run of
                           // this (parity, chain), coalesced like the block slots
       const int nrun = g.units_per_rank * NS;
-      for (int e = tid; e < g.world_size * nrun; e += NT) {
+      for (int e = rt; rt >= 0 && e < g.world_size * nrun; e += NT - 64) {
         const int q = e / nrun;
         if (q != a.rank) st_sys((double*)mb + (int64_t)q * per_rank + (e - q * nrun), slot_empty());
       }

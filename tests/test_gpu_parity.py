@@ -332,7 +332,9 @@ def test_clock_record_persistent_and_launch_per_sweep(L):
                 assert ghz == 0.0
                 continue
             assert 0.5 < ghz < 2.6
-            assert abs(probe / ghz - 1) < 0.1  # the two readings of one clock
+            # the two readings of one clock, the probe a moment after the run and under a lighter load
+            # (measured 2.17 record vs 2.35 probe on one box, 2.38-2.41 vs 2.34-2.35 on others)
+            assert abs(probe / ghz - 1) < 0.2
             s.run(1500)  # longer than the record (the last 1024 sweeps)
             assert 0.5 < s.clock_ghz() < 2.6
 
