@@ -253,24 +253,54 @@ def cpu_baseline(workload: str, warm: int = 20, timed: int = 200, parallel: bool
     return res
 
 
-def settle_clocks(ms: float, device: int) -> float:
-    """Hold the GPU busy for `ms` of wall time with fp64 matmuls (work unrelated to the sampler,
-    outside every timed region), so that a short timed window runs at the clocks a whole run sees:
-    the driver's 20-sweep window after 5 one-sweep warm-up calls otherwise starts from the idle
-    power state and pays ~0.85 us per sweep of clock ramp (tools/driver_breakdown.py, cases cold /
-    after_busy / after_long / long_then_idle: profiles/r04_clock_ramp.jsonl).  Returns the seconds
-    spent."""
+def settle_clocks(ms: float, device: int, scratch=None) -> float:
+    """Hold the GPU busy for `ms` of wall time outside every timed region, so that a short timed
+    window runs at the clocks a whole run sees: the driver's 20-sweep window after 5 one-sweep
+    warm-up calls otherwise starts from the idle power state and pays ~0.85 us per sweep of clock
+    ramp (tools/driver_breakdown.py, cases cold / after_busy / after_long / long_then_idle:
+    profiles/r04_clock_ramp.jsonl).  `scratch`: a sampler of its own over the same customers
+    (scratch_sampler) whose sweeps are the busy work — the clock the governor settles at depends on
+    the load, and fp64 matmuls (the fallback without one) left the c2 window at 2.25 GHz against
+    the 2.38 of a whole run of sweeps.  The timed sampler's chains are untouched.
+    Returns the seconds spent."""
     import torch
     if ms <= 0:
         return 0.0
+    t0 = time.perf_counter()
+    if scratch is not None:
+        n = 16
+        while True:
+            t1 = time.perf_counter()
+            scratch.run(n)
+            scratch.synchronize()
+            torch.cuda.synchronize()
+            now = time.perf_counter()
+            if now - t0 >= ms / 1e3:
+                break
+            n = max(1, min(4 * n, 4096, int(n * 2e-3 / max(now - t1, 1e-6))))  # ~2 ms per call
+        return time.perf_counter() - t0
     a = torch.randn(2048, 2048, dtype=torch.float64, device=f"cuda:{device}")
     b = a
-    t0 = time.perf_counter()
     while time.perf_counter() - t0 < ms / 1e3:
         b = torch.tanh(a @ b * 1e-3)
         torch.cuda.synchronize()
     del a, b
     return time.perf_counter() - t0
+
+
+SETTLE_WORK = "sampler"  # --settle-work (A/B: "matmul" = the fp64 matmuls of rounds 4-5)
+
+
+def scratch_sampler(p, chains: int, device: int):
+    """The clock-settle work of a leg (settle_clocks): a world-size-1 sampler over the same customers
+    (at N > 1 the rank's own shard), seed 7, no draws kept — the same kernel family as the timed
+    sampler, its own handle, state and stream.  None where it cannot be built (its memory)."""
+    from mcmc_clv_model_amd.sampler import HipSampler
+    try:
+        return HipSampler(p, mcmc=1, burnin=10 ** 8, thin=1, chains=chains, seed=7, draw_sink="none",
+                          device=device)
+    except Exception:
+        return None
 
 
 def profile_name(workload: str, phase: str) -> str:
@@ -377,6 +407,13 @@ def run_leg(name: str, world: int, rank: int, local_rank: int, dist, steps: int,
                               draw_sink=sink, device=local_rank, graph_chunk=graph_chunk,
                               exchange=exchange if world > 1 else "rccl", verify_sweeps=8)
         run, sync = kern.step, kern.synchronize
+    scratch = None
+    if settle_ms > 0 and SETTLE_WORK == "sampler":
+        if sharded:
+            from mcmc_clv_model_amd.distributed import slice_problem
+            scratch = scratch_sampler(slice_problem(p, *kern.plan.shard(rank)), chains, local_rank)
+        else:
+            scratch = scratch_sampler(p, chains, local_rank)
     del p
     info = kern.launch_info()
     persistent = info["persistent"]
@@ -458,7 +495,7 @@ def run_leg(name: str, world: int, rank: int, local_rank: int, dist, steps: int,
             r["hyper_kernel_us"] = round(kt["hyper_ms"] / kt["hyper_launches"] * 1e3, 3)
         return r
 
-    settle_s = settle_clocks(settle_ms, local_rank)  # (the problem build left the GPU idle for seconds)
+    settle_s = settle_clocks(settle_ms, local_rank, scratch)  # (the problem build left the GPU idle for seconds)
     if persistent and one_call_warmup:  # the warm-up steps one call each, through the timed path (events
         kern.set_timing(True)           # on): the timed call is not the process's first of its kind
         for _ in range(warmup):
@@ -522,7 +559,7 @@ def run_leg(name: str, world: int, rank: int, local_rank: int, dist, steps: int,
         # (warm), then `steps` stored sweeps
         run(burnin + 100 - done)
         sync()
-        settle_clocks(settle_ms, local_rank)
+        settle_clocks(settle_ms, local_rank, scratch)
         dt_st, kt_st = timed(steps, persistent)
         clk_st, clk_st_src, _ = run_clock()
         first = burnin + 101
@@ -563,6 +600,10 @@ def run_leg(name: str, world: int, rank: int, local_rank: int, dist, steps: int,
                             f"torch.cuda graph replay ({graph_chunk} sweeps: sweep + group kernels, RCCL all_gather, "
                             "level-2 kernel)" if graph_chunk else "eager: sweep + group kernels, RCCL all_gather, level-2")
     kern.close()
+    if scratch is not None:
+        scratch.close()
+    res["clock_settle_work"] = ("sweeps of a scratch sampler over the same customers (seed 7, no draws kept)"
+                                if scratch is not None else "fp64 matmuls" if settle_ms > 0 else None)
     return res
 
 
@@ -592,6 +633,9 @@ def main():
     ap.add_argument("--phase", default="burnin", choices=["burnin", "stored"],
                     help="(profiling) stored: the sampler's burn-in is 0, so every timed sweep is a stored sweep "
                          "(the running sums' read-modify-write / the draws' stores of bi:402-428)")
+    ap.add_argument("--settle-work", default="sampler", choices=["sampler", "matmul"],
+                    help="the clock-settle work before each timed window (settle_clocks): sweeps of a scratch "
+                         "sampler over the same customers, or fp64 matmuls (A/B)")
     ap.add_argument("--no-c1-leg", dest="c1_leg", action="store_false",
                     help="skip BASELINE configs[0] (c1 on the GPU and its 1-core CPU leg)")
     ap.add_argument("--no-stored-phase", dest="stored_phase", action="store_false",
@@ -608,6 +652,8 @@ def main():
     ap.add_argument("--cpu-warm", type=int, default=20)
     ap.add_argument("--cpu-timed", type=int, default=200)
     a = ap.parse_args()
+    global SETTLE_WORK
+    SETTLE_WORK = a.settle_work
     if a.cpu_baseline_child:
         cpu_baseline_child(a.workload or "c2", a.cpu_warm, a.cpu_timed)
         return
@@ -697,8 +743,8 @@ def main():
             n_gpus=world, steps=a.steps, warmup=a.warmup, ms_per_step=prim["ms_per_step"], higher_is_better=True,
             scaling="weak", vs_baseline=None, dtype="f64",
             proposal_dtype="f32",  # t3 proposal noise and accept log-uniforms; state, posterior f64
-            ms_per_step_kind=("steady state: the GPU's clocks settled by clock_settle_ms of unrelated work before the "
-                              "warm-up; the timed call leaves its last level-2 draw pending (drawn at the start of the "
+            ms_per_step_kind=("steady state: the GPU's clocks settled by clock_settle_ms of sweeps on a scratch sampler "
+                              "(clock_settle_work; the timed chains untouched) before the warm-up; the timed call leaves its last level-2 draw pending (drawn at the start of the "
                               "next call) — `cold` times the same steps from an idle GPU with that draw included")
             if prim.get("_persistent") and not sharded else "wall time of the timed steps",
             data=(f"synthetic CBS ({n_total} customers, mcmc_clv_model_amd.data.synthetic_cbs" +
@@ -713,6 +759,7 @@ def main():
                         **({"phase": "stored (profiling: burn-in 0, every sweep stores)"} if a.phase == "stored" else {}),
                         timed_region=prim["_timed_region"]),
             clock_settle_ms=prim["clock_settle_ms"],
+            clock_settle_work=prim.get("clock_settle_work"),
             gpu_clock_ghz=prim.get("gpu_clock_ghz"),
             gpu_clock_source=prim.get("gpu_clock_source"),
             gpu_clock_probe_ghz=prim.get("gpu_clock_probe_ghz"),

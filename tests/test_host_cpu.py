@@ -625,6 +625,67 @@ def test_bench_config_times_the_stored_phase(monkeypatch):
     assert [(a, b) for a, b, _ in log] == [(1, 200), (201, 1200), (1201, 2200)] and "stored" not in r1
 
 
+def test_bench_clock_settle_runs_a_scratch_sampler(monkeypatch):
+    """The clock settle before each timed window sweeps a scratch sampler of its own (seed 7, no draws
+    kept) over the same customers: the timed sampler runs exactly the warm-up and the timed steps,
+    the scratch is closed with the leg, and the line names the settle work.  Stub samplers, no GPU."""
+    import torch
+
+    import bench
+    from mcmc_clv_model_amd import sampler as S
+
+    made = []
+
+    class Fake:
+        n = 500
+
+        def __init__(self, p, **kw):
+            self.kw, self.log, self.closed = kw, [], False
+            made.append(self)
+
+        def run(self, n):
+            self.log.append(n)
+
+        def synchronize(self):
+            pass
+
+        def launch_info(self):
+            return dict(persistent=True)
+
+        def set_timing(self, on):
+            pass
+
+        def kernel_time(self):
+            return dict(sweep_ms=0.2, sweep_launches=20, hyper_ms=0.0, hyper_launches=0)
+
+        def clock_ghz(self):
+            return 2.38
+
+        def clock_probe(self, us):
+            return 2.4
+
+        def host_times(self):
+            return {}
+
+        def close(self):
+            self.closed = True
+
+    monkeypatch.setattr(S, "HipSampler", Fake)
+    monkeypatch.setattr(S, "build_problem", lambda df, covs, D: None)
+    monkeypatch.setattr(torch.cuda, "synchronize", lambda *a, **k: None)
+    r = bench.run_leg("c2", 1, 0, 0, None, 20, 5, settle_ms=5.0, stored_phase=False)
+    timed, scratch = made
+    assert timed.kw["seed"] == 42 and timed.log == [5, 20]  # warm-up, then exactly the timed steps
+    assert scratch.kw["seed"] == 7 and scratch.kw["draw_sink"] == "none" and scratch.kw["chains"] == timed.kw["chains"]
+    assert len(scratch.log) >= 1 and scratch.closed and timed.closed
+    assert r["clock_settle_ms"] >= 5.0 and r["clock_settle_work"].startswith("sweeps of a scratch sampler")
+    monkeypatch.setattr(bench, "SETTLE_WORK", "matmul")
+    monkeypatch.setattr(bench, "settle_clocks", lambda ms, dev, scratch=None: 0.005)
+    made.clear()
+    r = bench.run_leg("c2", 1, 0, 0, None, 20, 5, settle_ms=5.0, stored_phase=False)
+    assert len(made) == 1 and r["clock_settle_work"] == "fp64 matmuls"
+
+
 def test_bench_primary_is_a_baseline_configuration():
     """Verdict r4 #7: the line's `value` is a BASELINE configuration at every N — c2 (configs[1]) on
     one GPU, the 8-GPU weak-scaling c5 (configs[4]) at N > 1 — and the other configurations run as

@@ -1,12 +1,12 @@
-# Scratch GPU session script (overwritten per experiment; the round-6 diagnostics ran from it).
+# Scratch GPU session script (overwritten per experiment).
+# Round 6: the driver's command with the clock settled by the sampler's own sweeps vs fp64 matmuls.
 set -o pipefail
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out; export TMPDIR=/tmp
-L=$PWD/mcmc_clv_model_amd
-timeout -k 10 600 python -u -m pytest tests/test_gpu_p2p.py tests/test_gpu_parity.py -x -q -k "p2p or persistent or resume or sharded or clock" -p no:cacheprovider --timeout 200 --timeout-method thread > gpurun_out/c_tests.log 2>&1 || { tail -30 gpurun_out/c_tests.log; exit 1; }
-tail -2 gpurun_out/c_tests.log
-for rep in 1 2; do for lib in $PWD/build/head/libclvmcmc.so $L/libclvmcmc.so; do
-  CLV_LIB_PATH=$lib timeout -k 10 300 python tools/fx_ab.py 3 9 300000 2 300 2>&1 | grep "^{" || exit 1
-  CLV_LIB_PATH=$lib timeout -k 10 300 python tools/fx_ab.py 2 5 250000 2 300 2>&1 | grep "^{" || exit 1
-  CLV_PERSISTENT=1 CLV_LIB_PATH=$lib timeout -k 10 300 python tools/persist_breakdown.py c4_shard8 3000 > gpurun_out/c_wall.txt 2>&1 || exit 1
-  echo c4_shard8 $lib $(tail -1 gpurun_out/c_wall.txt)
+for rep in 1 2; do for w in sampler matmul; do
+  timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --settle-work $w > gpurun_out/drv_$w.log 2>&1 || { tail -20 gpurun_out/drv_$w.log; exit 1; }
+  python - $w <<'PY'
+import json,sys
+l=json.loads(open(f"gpurun_out/drv_{sys.argv[1]}.log").read().strip().splitlines()[-1])
+print(sys.argv[1], "value=%.4e" % l["value"], "us/step=%.3f" % (l["ms_per_step"]*1e3), "clk", l["gpu_clock_ghz"], "kernel_us/sweep", l["roofline"]["sweep_kernel_us"], "cold", round(l["cold"]["ms_per_step"]*1e3,2), "c4", round(l["configs"]["c4"]["ms_per_step"]*1e3,2), l["configs"]["c4"]["gpu_clock_ghz"])
+PY
 done; done
