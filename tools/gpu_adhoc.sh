@@ -1,12 +1,12 @@
 # Scratch GPU session script (overwritten per experiment).
-# Round 6: the driver's command with the clock settled by the sampler's own sweeps vs fp64 matmuls.
+# Round 6: the persistent level-2 workgroup's coalesced poll, group size 4 / 8 / all (build/gc8,
+# build/gc64) vs the lane-per-block poll (build/nocoal): wall us per sweep (persistent forced).
 set -o pipefail
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out; export TMPDIR=/tmp
-for rep in 1 2; do for w in sampler matmul; do
-  timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --settle-work $w > gpurun_out/drv_$w.log 2>&1 || { tail -20 gpurun_out/drv_$w.log; exit 1; }
-  python - $w <<'PY'
-import json,sys
-l=json.loads(open(f"gpurun_out/drv_{sys.argv[1]}.log").read().strip().splitlines()[-1])
-print(sys.argv[1], "value=%.4e" % l["value"], "us/step=%.3f" % (l["ms_per_step"]*1e3), "clk", l["gpu_clock_ghz"], "kernel_us/sweep", l["roofline"]["sweep_kernel_us"], "cold", round(l["cold"]["ms_per_step"]*1e3,2), "c4", round(l["configs"]["c4"]["ms_per_step"]*1e3,2), l["configs"]["c4"]["gpu_clock_ghz"])
-PY
+L=$PWD/mcmc_clv_model_amd/libclvmcmc.so
+for rep in 1 2; do for lib in $PWD/build/nocoal/libclvmcmc.so $L $PWD/build/gc8/libclvmcmc.so $PWD/build/gc64/libclvmcmc.so; do
+  for W in c4_shard8; do
+    CLV_PERSISTENT=1 CLV_LIB_PATH=$lib timeout -k 10 300 python tools/persist_breakdown.py $W 3000 > gpurun_out/c_wall.txt 2>&1 || { tail -5 gpurun_out/c_wall.txt; exit 1; }
+    echo $W $lib $(grep "wall:" gpurun_out/c_wall.txt)
+  done
 done; done
