@@ -299,8 +299,13 @@ def scratch_sampler(p, chains: int, device: int):
     try:
         return HipSampler(p, mcmc=1, burnin=10 ** 8, thin=1, chains=chains, seed=7, draw_sink="none",
                           device=device)
-    except Exception:
+    except Exception as e:  # (the line says so: clock_settle_work)
+        global SCRATCH_ERROR
+        SCRATCH_ERROR = f"{type(e).__name__}: {e}"[:200]
         return None
+
+
+SCRATCH_ERROR = None  # why the last scratch_sampler call returned None
 
 
 def profile_name(workload: str, phase: str) -> str:
@@ -603,7 +608,10 @@ def run_leg(name: str, world: int, rank: int, local_rank: int, dist, steps: int,
     if scratch is not None:
         scratch.close()
     res["clock_settle_work"] = ("sweeps of a scratch sampler over the same customers (seed 7, no draws kept)"
-                                if scratch is not None else "fp64 matmuls" if settle_ms > 0 else None)
+                                if scratch is not None else
+                                ("fp64 matmuls" + (f" (scratch sampler unavailable: {SCRATCH_ERROR})"
+                                                   if SETTLE_WORK == "sampler" and SCRATCH_ERROR else ""))
+                                if settle_ms > 0 else None)
     return res
 
 
