@@ -76,7 +76,12 @@ def main(tag, prof=os.path.join(ROOT, "gpurun_out", "prof"), bench_log=None, tra
             en = [int(t["End_Timestamp"]) for t in rows]
             k["median_gap_ns"] = statistics.median([st[i + 1] - en[i] for i in range(len(rows) - 1)])
         if "persist_kernel" in name:
-            if trace_sweeps and len(trace_sweeps) == len(rows):
+            if trace_sweeps and len(trace_sweeps) <= len(rows):
+                # the list names the bench's own dispatches, the last ones of the trace; earlier ones
+                # are the clock settle's scratch sampler (bench.settle_clocks, round 6), not counted
+                if len(rows) > len(trace_sweeps):
+                    k["settle_dispatches"] = len(rows) - len(trace_sweeps)
+                    rows = rows[len(rows) - len(trace_sweeps):]
                 k["dispatches"] = [dict(sweeps=n, ns=int(t["End_Timestamp"]) - int(t["Start_Timestamp"]),
                                         ns_per_sweep=(int(t["End_Timestamp"]) - int(t["Start_Timestamp"])) / n)
                                    for n, t in zip(trace_sweeps, rows)]
