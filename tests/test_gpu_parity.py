@@ -688,6 +688,35 @@ def test_persistent_kernel_bitwise_equals_launch_per_sweep(L, monkeypatch, D, co
             assert np.array_equal(bits(x), bits(y))
 
 
+def test_c4_eight_rank_shard_persistent_bitwise(L):
+    """The instance one GPU runs in c4's 8-rank run at its full size (rank 0's shard of the 1M-customer
+    K = 5 problem: 126,976 customers, 496 blocks; bench.py's c4_shard8 leg) at world size 1: the
+    persistent kernel — level-2 workgroup alone on a CU (>= 256 blocks), coalesced slot resets by
+    wavefronts 1-3 during the draw (round 6) — against one launch per sweep, bit for bit over uneven
+    clv_run calls through burn-in and stored sweeps (state, running sums, level-2 records,
+    log-likelihood)."""
+    from mcmc_clv_model_amd import distributed as Dm
+    from mcmc_clv_model_amd.data import synthetic_cbs
+    from mcmc_clv_model_amd.sampler import build_problem
+    full = build_problem(synthetic_cbs(1_000_000, 5, 2, seed=20250718), [f"c{k}" for k in range(1, 5)], 2)
+    plan = Dm.plan(full.N, 8)
+    b, e = plan.shard(0)
+    p = Dm.slice_problem(full, b, e)
+    assert p.N == 126_976
+    del full
+    kw = dict(mcmc=25, burnin=6, thin=3, chains=1, seed=2024, draw_sink="summary", n_mh_steps=20)
+    chunks = (1, 7, 2, 20, 1)
+    a = _run_mode(p, True, 31, chunks, **kw)
+    c = _run_mode(p, False, 31, chunks, **kw)
+    assert a[0]["persistent"] and not c[0]["persistent"], (a[0], c[0])
+    for x, y in zip(a[1], c[1]):
+        assert np.array_equal(bits(x), bits(y))
+    for x, y in zip(a[2:], c[2:]):
+        if x is not None:
+            assert np.array_equal(bits(x), bits(y))
+    assert np.isfinite(a[5]).all()  # the running sums
+
+
 def _run_ops(p, env, ops, **kw):
     """A sampler created under `env`, driven by `ops` ("run", n) / ("state",) / ("rollback",);
     returns the states taken at ("state",) ops, the final state and the draws."""
